@@ -1,0 +1,137 @@
+/* include/bchk.h -- C ABI of libbchk.so, the MI355X (gfx950) Kaneko/BCH soft decoder.
+ *
+ * This is the drop-in boundary for the reference's hot path. The reference has no FFI;
+ * its boundary is the C++ class API below, which the headers in include/bchk_dropin/ re-declare
+ * on top of these entry points. Each entry point names the
+ * reference interface it replaces (paths relative to the reference repo root).
+ *
+ * Conventions
+ *  - Every function returns 0 on success and a negative BCHK_E* code on failure;
+ *    bchk_last_error() describes the last failure of the calling thread. Nothing throws.
+ *  - One context = one (code, J, decoder SNR, device); it owns a HIP stream. A context
+ *    is not thread-safe; use one per host thread.
+ *  - Bit vectors are one byte per position (0/1), position i = coefficient of x^i,
+ *    exactly as the reference's unsigned char arrays.
+ *  - *_host functions take host pointers and are synchronous. *_device functions take
+ *    device pointers, enqueue on `stream` (a hipStream_t, NULL = the context's stream)
+ *    and return immediately.
+ *  - There is NO CPU fallback: without a usable gfx950 device every compute call fails
+ *    with BCHK_ENODEV.
+ */
+#ifndef BCHK_H
+#define BCHK_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BCHK_OK 0
+#define BCHK_EINVAL -1   /* bad argument / unsupported (m, t)                       */
+#define BCHK_ENODEV -2   /* no HIP device, or the gfx950 code object failed to load */
+#define BCHK_EHIP -3     /* a HIP runtime call failed                               */
+#define BCHK_ENOMEM -4
+
+/* J: the reference's test-pattern exponent cap.
+ *   BCHK_J_SHIPPED (-1): as shipped, `T = j` (src/KanekoKernelProcessor.cpp:393);
+ *   J >= 0: the commented-out `T = (j > J) ? J : j` (:392, J = 15 in the header :35). */
+#define BCHK_J_SHIPPED (-1)
+
+/* Decoder variants of KanekoKernelProcessor::decode */
+#define BCHK_VARIANT_ANSWER 0 /* decode(answer, word, res) :335-407 (used by fun())       */
+#define BCHK_VARIANT_WORD 1   /* decode(word, res)         :212-276 (main.cpp file mode)  */
+
+/* per-codeword flags (bchk_stats.flags) */
+#define BCHK_F_ACCEPTED 1u   /* res was written (else the row is left untouched)       */
+#define BCHK_F_RETURNED 2u   /* left through `l < calcRightSide()` (:380-382)          */
+#define BCHK_F_TRUNCATED 4u  /* stopped at the context's max_decodes safety cap:        */
+                             /* result is NOT the reference's                           */
+#define BCHK_F_TIE 8u        /* two |alpha| exactly equal: std::sort order unspecified  */
+#define BCHK_F_SCAN_UB 16u   /* VARIANT_WORD only: the unbounded calcT scan (:257)      */
+                             /* would read past alphaSorted[n-1] (UB in the reference)  */
+
+typedef struct bchk_stats {
+    uint64_t decodes;      /* += decodingCount                                (:368) */
+    uint64_t comparisons;  /* += comparisonCount                       (:387,396,402) */
+    uint64_t sums;         /* += summCount                                 (:388,403) */
+    uint64_t iterations;   /* completed loop iterations                               */
+    uint64_t jsteps;       /* calcT scan steps                                        */
+    uint64_t improvements; /* accepted candidates that did not return                 */
+    uint32_t flags;        /* BCHK_F_*                                                */
+    uint32_t reserved;
+} bchk_stats;
+
+typedef struct bchk_ctx bchk_ctx;
+
+/* Replaces KanekoKernelProcessor::KanekoKernelProcessor(pw, n, t, k, antilog, log, snr)
+ * (headers/KanekoKernelProcessor.h:47-50, src/KanekoKernelProcessor.cpp:17-26) plus the
+ * GF/generator setup of src/main.cpp:59-93. Supported: 2 <= m <= 8, 1 <= t <= 32,
+ * t < 2^(m-1) (main.cpp:55). decoder_snr_db is 0.5 in every reference call site. */
+int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx **out);
+void bchk_destroy(bchk_ctx *ctx);
+
+/* n, k (= n - deg g, main.cpp:93) and deg g + 1. */
+int bchk_code_params(const bchk_ctx *ctx, int *n, int *k, int *gsize);
+/* g(x) coefficients low -> high (gsize bytes), as printVec(g, gSize) in main.cpp:95. */
+int bchk_generator(const bchk_ctx *ctx, uint8_t *g);
+/* Safety cap on algebraic decodes per codeword (0 = unlimited, the default). Codewords
+ * that hit it are flagged BCHK_F_TRUNCATED. */
+int bchk_set_max_decodes(bchk_ctx *ctx, uint64_t max_decodes);
+
+/* Replaces KanekoKernelProcessor::decode(answer, word, res)
+ * (headers/KanekoKernelProcessor.h:55, src/KanekoKernelProcessor.cpp:335-407), batched:
+ *   y   [B][n] channel samples (double), row b = `word` of codeword b
+ *   res [B][n] decoded words; row b is written only if flags & BCHK_F_ACCEPTED
+ *   l0  [B]    path metric of res (calcL(res)), DBL_MAX if not accepted   (may be NULL)
+ *   st  [B]    counters / flags                                           (may be NULL)
+ * `answer` is not an input: the reference ignores it (:345 computes an unused value). */
+int bchk_decode_host(bchk_ctx *ctx, const double *y, size_t B, uint8_t *res, double *l0,
+                     bchk_stats *st);
+int bchk_decode_device(bchk_ctx *ctx, const double *d_y, size_t B, uint8_t *d_res,
+                       double *d_l0, bchk_stats *d_st, void *stream);
+/* As above for another decode() variant (BCHK_VARIANT_*). */
+int bchk_decode_variant_host(bchk_ctx *ctx, int variant, const double *y, size_t B,
+                             uint8_t *res, double *l0, bchk_stats *st);
+
+/* Replaces Decoder::decode(word, answer) (headers/Decoder.h:78, src/Decoder.cpp:298-321),
+ * batched. The reference decodes from its stored syndrome (findSyndromPoly/
+ * alterSyndromPoly, src/Decoder.cpp:184-230) and flips bits of `word`; syndromes (may be
+ * NULL) carries that stored state as the t odd syndromes S_1, S_3, ..., S_{2t-1} per word
+ * ([N][t] GF elements as uint32). NULL = syndromes of `words` themselves.
+ *   ok [N] 1 on success; answers [N][n] written only where ok. */
+int bchk_alg_decode_host(bchk_ctx *ctx, const uint8_t *words, const uint32_t *syndromes,
+                         size_t N, uint8_t *answers, uint8_t *ok);
+
+/* FER/BER/op-counter accumulation of one batch (src/dataForPlot.cpp:55-74), on device:
+ *   out6 += {frame errors, bit errors, decodes, comparisons, sums, words}
+ * tx/res [B][n]; st [B] from bchk_decode_device. d_out6 is a device uint64_t[6]. */
+int bchk_count_device(bchk_ctx *ctx, const uint8_t *d_tx, const uint8_t *d_res,
+                      const bchk_stats *d_st, size_t B, uint64_t *d_out6, void *stream);
+
+/* The reference's input stream (src/bchCoder.cpp:228-250 in fun() order): minstd_rand0
+ * seeded with `seed`, B words at Eb/N0 snr_db: tx [B][n], y [B][n]. rng_state (in/out,
+ * may be NULL) is the engine state: pass 0 to start from `seed`. Host-side, sequential. */
+int bchk_generate_host(const bchk_ctx *ctx, double snr_db, size_t B, uint64_t *rng_state,
+                       uint64_t seed, uint8_t *tx, double *y);
+
+/* fun(file, decoder, g, gSize, p, e, maxSTNR) (headers/dataForPlot.h:8,
+ * src/dataForPlot.cpp:16-116) on the GPU: identical CSV text, written to csv (cap bytes,
+ * NUL-terminated). batch = codewords decoded per GPU launch (0 = auto). */
+int bchk_sweep(bchk_ctx *ctx, long p, long e, double max_snr, uint64_t seed, size_t batch,
+               char *csv, size_t cap);
+
+int bchk_sync(bchk_ctx *ctx);
+/* the context's HIP stream (hipStream_t) */
+void *bchk_stream(bchk_ctx *ctx);
+/* Average duration (ms) of the search kernel over the last *_device calls made with
+ * bchk_profile(ctx, 1) enabled (HIP events recorded on the launch stream). */
+int bchk_profile(bchk_ctx *ctx, int enable);
+int bchk_profile_read(bchk_ctx *ctx, double *total_ms, uint64_t *launches);
+const char *bchk_last_error(void);
+const char *bchk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

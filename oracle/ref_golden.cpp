@@ -14,6 +14,8 @@
 //       the getters (headers/KanekoKernelProcessor.h:63-68).
 //   file <m> <t> <path>
 //       The known-answer word of in/infile.txt, decoded with decode(answer, y, res).
+//   bench <m> <t> <seed> <count> <snr_db>
+//       CPU-baseline timing of decode(answer, word, res) over `count` stream words.
 //   algdec <m> <t> exhaustive
 //       Decoder::decode (src/Decoder.cpp:298) on every coset representative of the
 //       cyclic code (every word supported on positions 0..n-k-1).
@@ -28,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <random>
 #include <string>
 #include <vector>
@@ -153,6 +156,35 @@ static int mode_file(long m, long t, const char *path) {
     return 0;
 }
 
+// bench <m> <t> <seed> <count> <snr_db>: CPU baseline timing. Generates `count` words of
+// the stream first, then times only the decode(answer, word, res) calls (one core).
+static int mode_bench(long m, long t, unsigned long seed, long count, double snr) {
+    Code c = make_code(m, t);
+    const long n = c.n, k = c.k;
+    generator.seed(seed);
+    KanekoKernelProcessor dec(m, n, t, k, c.alog, c.log, 0.5);
+    std::vector<unsigned char> info(k), tx(n * count), out(n);
+    std::vector<double> y(n * count);
+    double sd = sqrt(1 / (pow(10, snr / 10) * 2 * dec.getK() / dec.getN()));
+    for (long w = 0; w < count; ++w) {
+        generateRandomPoly(info.data(), k);
+        multiplyPolynomials(info.data(), (int)k, c.g, c.gSize, &tx[w * n]);
+        addNoise(sd, &tx[w * n], &y[w * n], n);
+    }
+    long errs = 0;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (long w = 0; w < count; ++w) {
+        dec.decode(&tx[w * n], &y[w * n], out.data());
+        errs += memcmp(out.data(), &tx[w * n], n) != 0;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    double el = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+    printf("{\"words\": %ld, \"seconds\": %.6f, \"codewords_per_s\": %.3f, \"decodes\": %lu, "
+           "\"frame_errors\": %ld}\n", count, el, count / el, dec.getDecodingCount(), errs);
+    return 0;
+}
+
 static uint64_t splitmix(uint64_t &s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ULL);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -198,6 +230,9 @@ int main(int argc, char **argv) {
     if (argc >= 7 && !strcmp(argv[1], "vectors"))
         return mode_vectors(atol(argv[2]), atol(argv[3]), strtoul(argv[4], 0, 10),
                             atol(argv[5]), atof(argv[6]));
+    if (argc >= 7 && !strcmp(argv[1], "bench"))
+        return mode_bench(atol(argv[2]), atol(argv[3]), strtoul(argv[4], 0, 10), atol(argv[5]),
+                          atof(argv[6]));
     if (argc >= 5 && !strcmp(argv[1], "file"))
         return mode_file(atol(argv[2]), atol(argv[3]), argv[4]);
     if (argc >= 5 && !strcmp(argv[1], "algdec"))

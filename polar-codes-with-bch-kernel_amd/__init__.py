@@ -1,0 +1,201 @@
+"""bchk_amd -- Python view of libbchk.so (MI355X Kaneko/BCH soft decoder), via ctypes.
+
+The product is the C ABI in include/bchk.h (HIP kernels for gfx950 + C++ host runtime);
+this module only marshals numpy arrays / device pointers for tests, bench.py and
+__graft_entry__. It mirrors the reference's KanekoKernelProcessor / Decoder / fun()
+surface (headers/KanekoKernelProcessor.h:47-68, headers/Decoder.h:67-78,
+headers/dataForPlot.h:8) with batched calls. There is no CPU fallback: if the HIP library
+or a gfx950 device is missing, constructing a KanekoKernelProcessor raises.
+
+Load it by path (the directory name is not an identifier):
+    spec = importlib.util.spec_from_file_location("bchk_amd", ".../__init__.py")
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libbchk.so")
+
+BCHK_J_SHIPPED = -1
+VARIANT_ANSWER, VARIANT_WORD = 0, 1
+F_ACCEPTED, F_RETURNED, F_TRUNCATED, F_TIE, F_SCAN_UB = 1, 2, 4, 8, 16
+
+# Every exported entry point of include/bchk.h.
+EXPORTS = (
+    "bchk_create", "bchk_destroy", "bchk_code_params", "bchk_generator",
+    "bchk_set_max_decodes", "bchk_decode_host", "bchk_decode_device",
+    "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device",
+    "bchk_generate_host", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
+    "bchk_profile_read", "bchk_last_error", "bchk_version",
+)
+
+STATS_DTYPE = np.dtype([("decodes", "<u8"), ("comparisons", "<u8"), ("sums", "<u8"),
+                        ("iterations", "<u8"), ("jsteps", "<u8"), ("improvements", "<u8"),
+                        ("flags", "<u4"), ("reserved", "<u4")])
+
+
+class BchkError(RuntimeError):
+    pass
+
+
+def build(force=False):
+    """Compile libbchk.so in-tree (hipcc --offload-arch=gfx950)."""
+    if force or not os.path.exists(LIB_PATH):
+        jobs = os.environ.get("MAX_JOBS", "8")
+        subprocess.run(["make", "-s", "-C", PKG_DIR, f"-j{min(int(jobs), 16)}"], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    """Load libbchk.so. If torch is importable it is imported first so that one HIP
+    runtime (torch's libamdhip64.so.7) serves both torch and libbchk in this process."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BchkError(f"{LIB_PATH} missing: run make -C {PKG_DIR} (no CPU fallback)")
+    if "torch" not in sys.modules and os.environ.get("BCHK_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
+    L = C.CDLL(LIB_PATH)
+    vp, sz, i32, u64, dbl = C.c_void_p, C.c_size_t, C.c_int, C.c_uint64, C.c_double
+    L.bchk_create.argtypes = [i32, i32, i32, dbl, i32, C.POINTER(vp)]
+    L.bchk_destroy.argtypes = [vp]
+    L.bchk_destroy.restype = None
+    L.bchk_code_params.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
+    L.bchk_generator.argtypes = [vp, vp]
+    L.bchk_set_max_decodes.argtypes = [vp, u64]
+    L.bchk_decode_host.argtypes = [vp, vp, sz, vp, vp, vp]
+    L.bchk_decode_device.argtypes = [vp, vp, sz, vp, vp, vp, vp]
+    L.bchk_decode_variant_host.argtypes = [vp, i32, vp, sz, vp, vp, vp]
+    L.bchk_alg_decode_host.argtypes = [vp, vp, vp, sz, vp, vp]
+    L.bchk_count_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
+    L.bchk_generate_host.argtypes = [vp, dbl, sz, C.POINTER(u64), u64, vp, vp]
+    L.bchk_sweep.argtypes = [vp, C.c_long, C.c_long, dbl, u64, sz, C.c_char_p, sz]
+    L.bchk_sync.argtypes = [vp]
+    L.bchk_stream.argtypes = [vp]
+    L.bchk_stream.restype = vp
+    L.bchk_profile.argtypes = [vp, i32]
+    L.bchk_profile_read.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
+    L.bchk_last_error.restype = C.c_char_p
+    L.bchk_version.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise BchkError(f"bchk error {rc}: {lib().bchk_last_error().decode()}")
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class KanekoKernelProcessor:
+    """Batched KanekoKernelProcessor (headers/KanekoKernelProcessor.h:47-68) for one
+    BCH(n, k) code with t = designed correction capability, on one gfx950 device."""
+
+    def __init__(self, m, t, J=BCHK_J_SHIPPED, decoder_snr_db=0.5, device=0):
+        L = lib()
+        h = C.c_void_p()
+        _check(L.bchk_create(m, t, J, decoder_snr_db, device, C.byref(h)))
+        self._h = h
+        n, k, gs = C.c_int(), C.c_int(), C.c_int()
+        _check(L.bchk_code_params(h, C.byref(n), C.byref(k), C.byref(gs)))
+        self.m, self.t, self.J = m, t, J
+        self.n, self.k = n.value, k.value
+        self.g = np.zeros(gs.value, np.uint8)
+        _check(L.bchk_generator(h, _p(self.g)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().bchk_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_max_decodes(self, md):
+        _check(lib().bchk_set_max_decodes(self._h, int(md)))
+
+    def decode(self, y, res=None, variant=VARIANT_ANSWER):
+        """y [B, n] f64 -> (res [B, n] u8, l0 [B] f64, stats [B] STATS_DTYPE).
+        Rows that are never accepted keep the incoming `res` content (default 0)."""
+        y = np.ascontiguousarray(np.atleast_2d(y), np.float64)
+        B = y.shape[0]
+        assert y.shape[1] == self.n
+        res = np.zeros((B, self.n), np.uint8) if res is None else np.ascontiguousarray(res, np.uint8)
+        l0 = np.zeros(B, np.float64)
+        st = np.zeros(B, STATS_DTYPE)
+        _check(lib().bchk_decode_variant_host(self._h, variant, _p(y), B, _p(res), _p(l0), _p(st)))
+        return res, l0, st
+
+    def decode_device(self, d_y, B, d_res, d_l0, d_st, stream=None):
+        _check(lib().bchk_decode_device(self._h, C.c_void_p(d_y), B, C.c_void_p(d_res),
+                                        C.c_void_p(d_l0), C.c_void_p(d_st),
+                                        C.c_void_p(stream) if stream else None))
+
+    def count_device(self, d_tx, d_res, d_st, B, d_out6, stream=None):
+        _check(lib().bchk_count_device(self._h, C.c_void_p(d_tx), C.c_void_p(d_res),
+                                       C.c_void_p(d_st), B, C.c_void_p(d_out6),
+                                       C.c_void_p(stream) if stream else None))
+
+    def alg_decode(self, words, syndromes=None):
+        """Decoder::decode batch: words [N, n] u8 -> (ok [N] bool, answers [N, n] u8)."""
+        words = np.ascontiguousarray(np.atleast_2d(words), np.uint8)
+        N = words.shape[0]
+        ans = np.zeros_like(words)
+        ok = np.zeros(N, np.uint8)
+        sp = None
+        if syndromes is not None:
+            syndromes = np.ascontiguousarray(syndromes, np.uint32)
+            sp = _p(syndromes)
+        _check(lib().bchk_alg_decode_host(self._h, _p(words), sp, N, _p(ans), _p(ok)))
+        return ok.astype(bool), ans
+
+    def generate(self, snr_db, B, seed=1, state=0):
+        """The reference input stream: (tx [B, n] u8, y [B, n] f64, next_state)."""
+        tx = np.zeros((B, self.n), np.uint8)
+        y = np.zeros((B, self.n), np.float64)
+        st = C.c_uint64(state)
+        _check(lib().bchk_generate_host(self._h, snr_db, B, C.byref(st), seed, _p(tx), _p(y)))
+        return tx, y, st.value
+
+    def sweep(self, p, e, max_snr=5.0, seed=1, batch=0):
+        """fun() on the GPU: the reference CSV text."""
+        buf = C.create_string_buffer(1 << 16)
+        _check(lib().bchk_sweep(self._h, p, e, max_snr, seed, batch, buf, len(buf)))
+        return buf.value.decode()
+
+    def sync(self):
+        _check(lib().bchk_sync(self._h))
+
+    @property
+    def stream(self):
+        return lib().bchk_stream(self._h)
+
+    def profile(self, enable=True):
+        _check(lib().bchk_profile(self._h, 1 if enable else 0))
+
+    def profile_read(self):
+        ms, n = C.c_double(), C.c_uint64()
+        _check(lib().bchk_profile_read(self._h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+def version():
+    return lib().bchk_version().decode()

@@ -1,0 +1,55 @@
+// bchk_device.h -- structures shared by the host runtime (bchk_host.cpp) and the gfx950
+// kernels (bchk_kernels.hip). Plain C++, no HIP types.
+#pragma once
+#include <stdint.h>
+
+#include "bchk.h"
+
+namespace bchk {
+
+constexpr int kMaxM = 8;
+constexpr int kMaxT = 32;
+constexpr int kWaveSize = 64;
+constexpr int kWavesPerBlock = 4;
+
+// Per-code lookup tables, one device blob, copied into LDS by every workgroup.
+//   exp8 [4n]        alpha^i for i < 2n-1, 0 above (so log(0) = 2n-1 sums to 0)
+//   log16[2^m]       log_alpha(v); log16[0] = 2n-1
+//   col  [n][W]      odd-syndrome column of position p: byte j of word j/4 =
+//                    alpha^((2j+1) p mod n), j < t   (Decoder::alterSyndromPoly :210-230)
+//   chien[t+1][2^m][EW] (m <= 6 only) bit-planes of v * alpha^(j k) over k = 0..n-1:
+//                    the Chien search of Decoder::locatorsAndRoots (:279-296) as a
+//                    GF(2)-linear map, XOR of t+1 table rows.
+struct TableDesc {
+    uint32_t off_exp, off_log, off_col, off_chien, bytes;
+    int32_t W;   // u32 words per packed odd-syndrome vector
+    int32_t EW;  // u64 words per Chien table row
+};
+
+struct SearchParams {
+    const double *y;       // [B][n]
+    uint8_t *res;          // [B][n]
+    double *l0;            // [B] or null
+    bchk_stats *st;        // [B] or null
+    const uint8_t *tables; // device blob, TableDesc layout
+    TableDesc td;
+    double s2;             // pow(sd0, 2), host glibc (src/KanekoKernelProcessor.cpp:337)
+    uint64_t max_decodes;  // 0 = unlimited
+    uint32_t count;        // codewords
+    int32_t t;
+    int32_t J;             // < 0: shipped
+    int32_t variant;       // BCHK_VARIANT_*
+};
+
+struct AlgParams {
+    const uint8_t *words;   // [N][n]
+    const uint32_t *synd;   // [N][t] or null
+    uint8_t *answers;       // [N][n]
+    uint8_t *ok;            // [N]
+    const uint8_t *tables;
+    TableDesc td;
+    uint32_t count;
+    int32_t t;
+};
+
+}  // namespace bchk

@@ -1,0 +1,558 @@
+// bchk_host.cpp -- host runtime of libbchk.so: code construction, device tables, kernel
+// dispatch and the batched Monte-Carlo sweep behind the C ABI in include/bchk.h.
+//
+// Reference behaviour it reproduces (paths relative to the reference repo root):
+//   GF(2^m) tables and g(x)       src/main.cpp:59-93, src/bchCoder.cpp:25-226
+//   input stream / channel        src/bchCoder.cpp:19-22, 228-250 (std::default_random_engine)
+//   FER sweep fun()               src/dataForPlot.cpp:16-116
+// All decoding runs on the GPU; there is no CPU decode path in this library.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "bchk.h"
+#include "bchk_device.h"
+#include "bchk_launch.h"
+
+
+using namespace bchk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(BCHK_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                        __FILE__, __LINE__);                                            \
+    } while (0)
+
+const unsigned kPrim[16] = {3, 7, 11, 19, 37, 67, 137, 285, 529, 1033,
+                            2053, 4179, 8219, 17475, 32771, 69643};  // main.cpp:14-15
+
+struct Field {
+    int m = 0, n = 0;
+    std::vector<unsigned> alog;  // alpha^i
+    std::vector<int> log;        // log(v), log(0) = -1
+    unsigned mul(unsigned a, unsigned b) const {
+        if (!a || !b) return 0;
+        int s = log[a] + log[b];
+        return alog[s >= n ? s - n : s];
+    }
+};
+
+Field make_field(int m) {
+    Field f;
+    f.m = m;
+    f.n = (1 << m) - 1;
+    f.alog.resize(f.n);
+    f.log.assign(f.n + 1, -1);
+    f.alog[0] = 1;
+    for (int i = 1; i < f.n; ++i) {
+        unsigned v = f.alog[i - 1] << 1;
+        if (v >> m) v ^= kPrim[m - 1];
+        f.alog[i] = v;
+    }
+    for (int i = 0; i < f.n; ++i) f.log[f.alog[i]] = i;
+    return f;
+}
+
+// g(x) = product of the distinct minimal polynomials of alpha^1 .. alpha^(2t-1)
+// (= their lcm, main.cpp:84-92), binary coefficients low -> high.
+std::vector<uint8_t> make_generator(const Field &f, int t) {
+    std::vector<uint8_t> g{1};
+    std::vector<bool> done(f.n, false);
+    for (int i = 1; i < 2 * t; ++i) {
+        const int i0 = i % f.n;
+        if (done[i0]) continue;
+        std::vector<unsigned> mp{1};
+        int e = i0;
+        do {
+            done[e] = true;
+            const unsigned root = f.alog[e];
+            std::vector<unsigned> nx(mp.size() + 1, 0);
+            for (size_t d = 0; d < mp.size(); ++d) {
+                nx[d + 1] ^= mp[d];
+                nx[d] ^= f.mul(mp[d], root);
+            }
+            mp.swap(nx);
+            e = (2 * e) % f.n;
+        } while (e != i0);
+        std::vector<uint8_t> prod(g.size() + mp.size() - 1, 0);
+        for (size_t a = 0; a < g.size(); ++a)
+            if (g[a])
+                for (size_t b = 0; b < mp.size(); ++b) prod[a + b] ^= (uint8_t)(mp[b] & 1u);
+        g.swap(prod);
+    }
+    return g;
+}
+
+// Device table blob (see TableDesc in bchk_device.h).
+std::vector<uint8_t> make_tables(const Field &f, int t, TableDesc *td) {
+    const int n = f.n, m = f.m;
+    const int W = (std::max(t, 1) + 3) / 4;
+    const int EW = (m + 1) & ~1;
+    auto align16 = [](size_t v) { return (v + 15) & ~size_t(15); };
+    size_t off = 0;
+    td->off_exp = (uint32_t)off;
+    off = align16(off + 4 * n);
+    td->off_log = (uint32_t)off;
+    off = align16(off + 2 * (size_t(1) << m));
+    td->off_col = (uint32_t)off;
+    off = align16(off + 4 * size_t(n) * W);
+    td->off_chien = (uint32_t)off;
+    if (m <= 6) off = align16(off + 8 * size_t(t + 1) * (size_t(1) << m) * EW);
+    td->bytes = (uint32_t)off;
+    td->W = W;
+    td->EW = EW;
+    std::vector<uint8_t> blob(off, 0);
+    uint8_t *ex = blob.data() + td->off_exp;
+    for (int i = 0; i < 2 * n - 1; ++i) ex[i] = (uint8_t)f.alog[i % n];
+    uint16_t *lg = reinterpret_cast<uint16_t *>(blob.data() + td->off_log);
+    lg[0] = (uint16_t)(2 * n - 1);
+    for (int v = 1; v <= n; ++v) lg[v] = (uint16_t)f.log[v];
+    uint32_t *col = reinterpret_cast<uint32_t *>(blob.data() + td->off_col);
+    for (int p = 0; p < n; ++p)
+        for (int j = 0; j < t; ++j) {
+            const unsigned s = f.alog[(size_t(2 * j + 1) * p) % n];
+            col[p * W + j / 4] |= s << (8 * (j % 4));
+        }
+    if (m <= 6) {
+        uint64_t *ch = reinterpret_cast<uint64_t *>(blob.data() + td->off_chien);
+        for (int j = 0; j <= t; ++j)
+            for (unsigned v = 0; v < (1u << m); ++v) {
+                uint64_t *row = ch + (size_t((j << m) + v)) * EW;
+                for (int k = 0; k < n; ++k) {
+                    const unsigned val = f.mul(v, f.alog[(size_t(j) * k) % n]);
+                    for (int b = 0; b < m; ++b)
+                        if ((val >> b) & 1u) row[b] |= 1ull << k;
+                }
+            }
+    }
+    return blob;
+}
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) return fail(BCHK_ENOMEM, "hipMalloc(%zu) failed", bytes);
+        cap = bytes;
+        return 0;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct bchk_ctx {
+    int m = 0, t = 0, n = 0, k = 0, J = -1, device = 0;
+    double decoder_snr_db = 0.5, s2 = 0.0;
+    Field field;
+    std::vector<uint8_t> g;
+    std::vector<uint8_t> tables_host;
+    TableDesc td{};
+    KernelSet ks{};
+    uint8_t *d_tables = nullptr;
+    hipStream_t stream = nullptr;
+    size_t lds = 0, lds_alg = 0;
+    int grid = 0;
+    uint64_t max_decodes = 0;
+    DevBuf y, res, l0, st, words, synd, ok;
+    bool profile = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    double prof_ms = 0.0;
+    uint64_t prof_launches = 0;
+};
+
+namespace {
+
+int sigma_s2(int k, int n, double snr_db, double *sd) {
+    // KanekoKernelProcessor ctor, src/KanekoKernelProcessor.cpp:20 (k, n are long there)
+    const long K = k, Nn = n;
+    *sd = sqrt(1 / (pow(10, snr_db / 10) * 2 * K / Nn));
+    return 0;
+}
+
+int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t *d_res,
+                  double *d_l0, bchk_stats *d_st, hipStream_t s) {
+    if (B == 0) return 0;
+    if (B > 0xFFFFFFFFull) return fail(BCHK_EINVAL, "batch too large");
+    SearchParams p{};
+    p.y = d_y;
+    p.res = d_res;
+    p.l0 = d_l0;
+    p.st = d_st;
+    p.tables = c->d_tables;
+    p.td = c->td;
+    p.s2 = c->s2;
+    p.max_decodes = c->max_decodes;
+    p.count = (uint32_t)B;
+    p.t = c->t;
+    p.J = c->J;
+    p.variant = variant;
+    const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
+    const int grid = std::max(1, std::min(c->grid, need));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->profile) {
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        HIP_TRY(hipEventRecord(e0, s));
+    }
+    HIP_TRY(launch_search(c->ks, p, grid, c->lds, s));
+    if (c->profile) {
+        HIP_TRY(hipEventRecord(e1, s));
+        c->events.emplace_back(e0, e1);
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *bchk_last_error(void) { return g_err.c_str(); }
+const char *bchk_version(void) { return "bchk 0.1 (gfx950)"; }
+
+int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx **out) {
+    if (!out) return fail(BCHK_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (m < 2 || m > kMaxM) return fail(BCHK_EINVAL, "m=%d unsupported (2..%d)", m, kMaxM);
+    if (t <= 0 || t >= (1 << (m - 1)) || t > kMaxT)
+        return fail(BCHK_EINVAL, "t=%d invalid for m=%d (1 <= t < 2^(m-1), t <= %d)", t, m, kMaxT);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(BCHK_ENODEV, "no HIP device visible (libbchk has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(BCHK_EINVAL, "device %d out of range", device);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(BCHK_ENODEV, "device %d is %s; libbchk is built for gfx950 only", device,
+                    prop.gcnArchName);
+    HIP_TRY(hipSetDevice(device));
+    bchk_ctx *c = new bchk_ctx();
+    c->m = m;
+    c->t = t;
+    c->J = J < 0 ? -1 : J;
+    c->device = device;
+    c->decoder_snr_db = decoder_snr_db;
+    c->field = make_field(m);
+    c->n = c->field.n;
+    c->g = make_generator(c->field, t);
+    c->k = c->n - (int)c->g.size() + 1;
+    double sd0;
+    sigma_s2(c->k, c->n, decoder_snr_db, &sd0);
+    c->s2 = pow(sd0, 2);  // src/KanekoKernelProcessor.cpp:337 `pow(sd, 2)`
+    if (!select_kernels(m, t, &c->ks)) {
+        delete c;
+        return fail(BCHK_EINVAL, "no kernel instantiated for m=%d t=%d", m, t);
+    }
+    c->tables_host = make_tables(c->field, t, &c->td);
+    int rc = 0;
+    if (hipMalloc(&c->d_tables, c->td.bytes) != hipSuccess ||
+        hipMemcpy(c->d_tables, c->tables_host.data(), c->td.bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        bchk_destroy(c);
+        return fail(BCHK_EHIP, "device setup failed: %s", hipGetErrorString(hipGetLastError()));
+    }
+    const size_t tb = (c->td.bytes + 15) & ~size_t(15);
+    c->lds = tb + kWavesPerBlock * c->ks.wave_bytes;
+    c->lds_alg = tb;
+    const void *fn = c->ks.search_ptr();
+    if (c->lds > 65536)
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveSize * kWavesPerBlock, c->lds) != hipSuccess ||
+        per_cu <= 0) {
+        per_cu = 1;
+        (void)hipGetLastError();
+    }
+    c->grid = per_cu * prop.multiProcessorCount;
+    (void)rc;
+    *out = c;
+    return 0;
+}
+
+void bchk_destroy(bchk_ctx *c) {
+    if (!c) return;
+    for (auto &e : c->events) {
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+    }
+    c->y.release();
+    c->res.release();
+    c->l0.release();
+    c->st.release();
+    c->words.release();
+    c->synd.release();
+    c->ok.release();
+    if (c->d_tables) hipFree(c->d_tables);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int bchk_code_params(const bchk_ctx *c, int *n, int *k, int *gsize) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    if (n) *n = c->n;
+    if (k) *k = c->k;
+    if (gsize) *gsize = (int)c->g.size();
+    return 0;
+}
+
+int bchk_generator(const bchk_ctx *c, uint8_t *g) {
+    if (!c || !g) return fail(BCHK_EINVAL, "NULL argument");
+    memcpy(g, c->g.data(), c->g.size());
+    return 0;
+}
+
+int bchk_set_max_decodes(bchk_ctx *c, uint64_t md) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    c->max_decodes = md;
+    return 0;
+}
+
+void *bchk_stream(bchk_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int bchk_sync(bchk_ctx *c) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int bchk_decode_device(bchk_ctx *c, const double *d_y, size_t B, uint8_t *d_res, double *d_l0,
+                       bchk_stats *d_st, void *stream) {
+    if (!c || (B && (!d_y || !d_res))) return fail(BCHK_EINVAL, "NULL argument");
+    return launch_search(c, BCHK_VARIANT_ANSWER, d_y, B, d_res, d_l0, d_st,
+                         stream ? (hipStream_t)stream : c->stream);
+}
+
+int bchk_decode_variant_host(bchk_ctx *c, int variant, const double *y, size_t B, uint8_t *res,
+                             double *l0, bchk_stats *st) {
+    if (!c || (B && (!y || !res))) return fail(BCHK_EINVAL, "NULL argument");
+    if (variant != BCHK_VARIANT_ANSWER && variant != BCHK_VARIANT_WORD)
+        return fail(BCHK_EINVAL, "unknown variant %d", variant);
+    if (B == 0) return 0;
+    const size_t n = c->n;
+    int rc;
+    if ((rc = c->y.ensure(B * n * sizeof(double))) || (rc = c->res.ensure(B * n)) ||
+        (rc = c->l0.ensure(B * sizeof(double))) || (rc = c->st.ensure(B * sizeof(bchk_stats))))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(c->y.p, y, B * n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    // rows that are never accepted must come back untouched
+    HIP_TRY(hipMemcpyAsync(c->res.p, res, B * n, hipMemcpyHostToDevice, c->stream));
+    if ((rc = launch_search(c, variant, (const double *)c->y.p, B, (uint8_t *)c->res.p,
+                            (double *)c->l0.p, (bchk_stats *)c->st.p, c->stream)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(res, c->res.p, B * n, hipMemcpyDeviceToHost, c->stream));
+    if (l0) HIP_TRY(hipMemcpyAsync(l0, c->l0.p, B * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (st) HIP_TRY(hipMemcpyAsync(st, c->st.p, B * sizeof(bchk_stats), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int bchk_decode_host(bchk_ctx *c, const double *y, size_t B, uint8_t *res, double *l0, bchk_stats *st) {
+    return bchk_decode_variant_host(c, BCHK_VARIANT_ANSWER, y, B, res, l0, st);
+}
+
+int bchk_alg_decode_host(bchk_ctx *c, const uint8_t *words, const uint32_t *synd, size_t N,
+                         uint8_t *answers, uint8_t *ok) {
+    if (!c || (N && (!words || !answers || !ok))) return fail(BCHK_EINVAL, "NULL argument");
+    if (N == 0) return 0;
+    if (N > 0xFFFFFFFFull) return fail(BCHK_EINVAL, "too many words");
+    const size_t n = c->n;
+    int rc;
+    if ((rc = c->words.ensure(N * n)) || (rc = c->res.ensure(N * n)) || (rc = c->ok.ensure(N)))
+        return rc;
+    if (synd && (rc = c->synd.ensure(N * c->t * sizeof(uint32_t)))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->words.p, words, N * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->res.p, answers, N * n, hipMemcpyHostToDevice, c->stream));
+    if (synd)
+        HIP_TRY(hipMemcpyAsync(c->synd.p, synd, N * c->t * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    AlgParams p{};
+    p.words = (const uint8_t *)c->words.p;
+    p.synd = synd ? (const uint32_t *)c->synd.p : nullptr;
+    p.answers = (uint8_t *)c->res.p;
+    p.ok = (uint8_t *)c->ok.p;
+    p.tables = c->d_tables;
+    p.td = c->td;
+    p.count = (uint32_t)N;
+    p.t = c->t;
+    HIP_TRY(launch_alg(c->ks, p, c->lds_alg, c->stream));
+    HIP_TRY(hipMemcpyAsync(answers, c->res.p, N * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ok, c->ok.p, N, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int bchk_count_device(bchk_ctx *c, const uint8_t *d_tx, const uint8_t *d_res, const bchk_stats *d_st,
+                      size_t B, uint64_t *d_out6, void *stream) {
+    if (!c || (B && (!d_tx || !d_res || !d_out6))) return fail(BCHK_EINVAL, "NULL argument");
+    if (B == 0) return 0;
+    HIP_TRY(launch_count(c->n, d_tx, d_res, d_st, (uint32_t)B, d_out6,
+                         stream ? (hipStream_t)stream : c->stream));
+    return 0;
+}
+
+// The reference's stream: std::default_random_engine (seed 1 unless RANDOM is defined,
+// src/bchCoder.cpp:14-22), uniform_int_distribution<unsigned short>(0, 1) for the
+// information bits and a fresh normal_distribution(0, sd) per addNoise call.
+static void gen_word(std::default_random_engine &eng, const bchk_ctx *c, double sd, uint8_t *tx,
+                     double *y, std::vector<uint8_t> &info) {
+    std::uniform_int_distribution<unsigned short> bit(0, 1);
+    for (int i = 0; i < c->k; ++i) info[i] = (uint8_t)bit(eng);
+    memset(tx, 0, c->n);
+    for (int i = 0; i < c->k; ++i)  // c(x) = info(x) g(x), bchCoder.cpp:120-132
+        if (info[i])
+            for (size_t j = 0; j < c->g.size(); ++j) tx[i + j] ^= c->g[j];
+    std::normal_distribution<double> noise(0.0, sd);
+    for (int i = 0; i < c->n; ++i) y[i] = (tx[i] ? 1 : -1) + noise(eng);
+}
+
+static double sweep_sigma(const bchk_ctx *c, double stnr) {
+    // src/dataForPlot.cpp:45 (getK()/getN() return long)
+    const long K = c->k, Nn = c->n;
+    return sqrt(1 / (pow(10, stnr / 10) * 2 * K / Nn));
+}
+
+int bchk_generate_host(const bchk_ctx *c, double snr_db, size_t B, uint64_t *rng_state, uint64_t seed,
+                       uint8_t *tx, double *y) {
+    if (!c || (B && (!tx || !y))) return fail(BCHK_EINVAL, "NULL argument");
+    std::default_random_engine eng(rng_state && *rng_state ? *rng_state : seed);
+    if (rng_state && *rng_state) {
+        std::stringstream ss;
+        ss << *rng_state;
+        ss >> eng;
+    }
+    std::vector<uint8_t> info(c->k);
+    const double sd = sweep_sigma(c, snr_db);
+    for (size_t b = 0; b < B; ++b) gen_word(eng, c, sd, tx + b * c->n, y + b * c->n, info);
+    if (rng_state) {
+        std::stringstream ss;
+        ss << eng;
+        ss >> *rng_state;
+    }
+    return 0;
+}
+
+int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t seed, size_t batch, char *csv,
+               size_t cap) {
+    if (!c || !csv || cap == 0) return fail(BCHK_EINVAL, "NULL argument");
+    if (p <= 0 || e <= 0) return fail(BCHK_EINVAL, "p and e must be positive");
+    const size_t n = c->n;
+    const size_t max_batch = batch ? batch : (size_t(1) << 18);
+    std::default_random_engine eng(seed);
+    std::vector<uint8_t> info(c->k), tx, res, dec(n, 0);
+    std::vector<double> y;
+    std::vector<bchk_stats> st;
+    std::vector<std::default_random_engine> snap;
+    std::ostringstream out;
+    int count = 0, countErr = 0, countE = 0;  // int, as src/dataForPlot.cpp:20
+    unsigned long D = 0, Cc = 0, Ss = 0, wordCount = 0;
+    double fer_est = 0.5;
+    for (double stnr = 0.0; stnr <= max_snr; stnr += 0.5) {
+        const double sd = sweep_sigma(c, stnr);
+        while (count < p && countErr < e) {
+            // batch size: enough words to reach e errors at the current estimate
+            const double want = 2.0 * (double)(e - countErr) / std::max(fer_est, 1e-7);
+            size_t nb = (size_t)std::min<double>(want, (double)max_batch);
+            nb = std::max<size_t>(nb, 256);
+            nb = std::min<size_t>(nb, (size_t)(p - count));
+            tx.resize(nb * n);
+            y.resize(nb * n);
+            res.assign(nb * n, 0);
+            st.resize(nb);
+            snap.resize(nb + 1);
+            for (size_t b = 0; b < nb; ++b) {
+                snap[b] = eng;
+                gen_word(eng, c, sd, &tx[b * n], &y[b * n], info);
+            }
+            snap[nb] = eng;
+            int rc = bchk_decode_host(c, y.data(), nb, res.data(), nullptr, st.data());
+            if (rc) return rc;
+            size_t used = 0;
+            int errs_batch = 0;
+            for (size_t b = 0; b < nb; ++b) {
+                if (!(count < p && countErr < e)) break;
+                if (st[b].flags & BCHK_F_ACCEPTED) memcpy(dec.data(), &res[b * n], n);
+                // else: the caller's buffer keeps the previous word's result (:25,52)
+                bool differ = memcmp(&tx[b * n], dec.data(), n) != 0;
+                if (differ) ++countErr, ++errs_batch;
+                for (size_t i = 0; i < n; ++i) countE += tx[b * n + i] != dec[i];
+                ++count;
+                ++wordCount;
+                D += st[b].decodes;
+                Cc += st[b].comparisons;
+                Ss += st[b].sums;
+                used = b + 1;
+            }
+            eng = snap[used];  // rewind the stream to the first word not consumed
+            fer_est = std::max(1e-7, (double)(errs_batch + 1) / (double)(used + 1));
+        }
+        out << stnr << "," << ((double)countErr) / count << "," << ((double)countE) / count / (long)n << ","
+            << ((double)D) / wordCount << "," << ((double)Cc) / wordCount << "," << ((double)Ss) / wordCount
+            << "\n";
+        D = Cc = Ss = 0;
+        wordCount = 0;
+        count = 0, countErr = 0;
+    }
+    const std::string s = out.str();
+    if (s.size() + 1 > cap) return fail(BCHK_EINVAL, "csv buffer too small (%zu needed)", s.size() + 1);
+    memcpy(csv, s.c_str(), s.size() + 1);
+    return 0;
+}
+
+int bchk_profile(bchk_ctx *c, int enable) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    c->profile = enable != 0;
+    return 0;
+}
+
+int bchk_profile_read(bchk_ctx *c, double *total_ms, uint64_t *launches) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    for (auto &e : c->events) {
+        HIP_TRY(hipEventSynchronize(e.second));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second));
+        c->prof_ms += ms;
+        c->prof_launches += 1;
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+    }
+    c->events.clear();
+    if (total_ms) *total_ms = c->prof_ms;
+    if (launches) *launches = c->prof_launches;
+    c->prof_ms = 0.0;
+    c->prof_launches = 0;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,24 @@
+// bchk_launch.h -- kernel dispatch table shared by bchk_kernels.hip and bchk_host.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "bchk_device.h"
+
+namespace bchk {
+
+struct KernelSet {
+    hipError_t (*search)(const SearchParams &, int, size_t, hipStream_t);
+    hipError_t (*alg)(const AlgParams &, size_t, hipStream_t);
+    const void *(*search_ptr)();
+    int tmax;
+    size_t wave_bytes;  // LDS bytes per wave of the search kernel
+};
+
+// Picks the (m, TMAX) instantiation for runtime t (smallest TMAX >= t).
+bool select_kernels(int m, int t, KernelSet *out);
+hipError_t launch_search(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s);
+hipError_t launch_alg(const KernelSet &k, const AlgParams &p, size_t lds, hipStream_t s);
+hipError_t launch_count(int n, const uint8_t *tx, const uint8_t *res, const bchk_stats *st,
+                        uint32_t B, uint64_t *out6, hipStream_t s);
+
+}  // namespace bchk

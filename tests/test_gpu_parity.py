@@ -1,0 +1,172 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors and
+the C oracle. Bit-exact on decoded words, path metrics (f64 bits) and counters."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from bchk_pkg import load
+from golden import GOLD, algdec_files, load_algdec, load_vectors, sweep_files, vector_files
+from oracle_lib import Oracle
+
+pytestmark = pytest.mark.gpu
+
+_ctx = {}
+
+
+def dec(m, t, J=-1):
+    key = (m, t, J)
+    if key not in _ctx:
+        _ctx[key] = load().KanekoKernelProcessor(m, t, J=J)
+    return _ctx[key]
+
+
+def check_against(v_res, v_l0, v_dec, v_cmp, v_sum, v_acc, res, l0, st):
+    F = load()
+    acc = (st["flags"] & F.F_ACCEPTED) != 0
+    np.testing.assert_array_equal(acc, v_acc.astype(bool))
+    np.testing.assert_array_equal(res[acc], v_res[acc])
+    np.testing.assert_array_equal(l0[acc].view(np.uint64), v_l0[acc].view(np.uint64))
+    np.testing.assert_array_equal(st["decodes"], v_dec)
+    np.testing.assert_array_equal(st["comparisons"], v_cmp)
+    np.testing.assert_array_equal(st["sums"], v_sum)
+    assert not np.any(st["flags"] & (F.F_TRUNCATED | F.F_TIE))
+
+
+@pytest.mark.parametrize("path", algdec_files(), ids=os.path.basename)
+def test_alg_decoder_matches_reference(path):
+    g = load_algdec(path)
+    d = dec(g.m, g.t)
+    ok, ans = d.alg_decode(g.words)
+    np.testing.assert_array_equal(ok, g.ok.astype(bool))
+    np.testing.assert_array_equal(ans[ok], g.answer[ok])
+
+
+def test_alg_decoder_from_stored_syndromes():
+    # Decoder::decode works from the stored syndrome, not from `word` (src/Decoder.cpp:298)
+    o = Oracle(6, 6)
+    d = dec(6, 6)
+    rng = np.random.default_rng(3)
+    tx, _ = o.stream(5, 64, 6.0)
+    err = (rng.random(tx.shape) < 0.05).astype(np.uint8)
+    words = tx ^ err
+    # syndromes of `words`, handed over explicitly; the decoder must flip bits of zeros
+    S = np.zeros((64, 6), np.uint32)
+    for b in range(64):
+        for j in range(6):
+            s = 0
+            for p in np.flatnonzero(words[b]):
+                s ^= o.code.alog[((2 * j + 1) * int(p)) % 63]
+            S[b, j] = s
+    ok1, a1 = d.alg_decode(words)
+    ok2, a2 = d.alg_decode(np.zeros_like(words), syndromes=S)
+    np.testing.assert_array_equal(ok1, ok2)
+    np.testing.assert_array_equal(a1[ok1] ^ words[ok1], a2[ok2])
+
+
+@pytest.mark.parametrize("path", vector_files(), ids=os.path.basename)
+def test_kaneko_matches_reference_vectors(path):
+    v = load_vectors(path)
+    d = dec(v.m, v.t)
+    assert (d.n, d.k) == (v.n, v.k)
+    np.testing.assert_array_equal(d.g, v.g)
+    res, l0, st = d.decode(v.y)
+    check_against(v.res, v.l0, v.decodes, v.cmp, v.sums, v.accepted, res, l0, st)
+
+
+def test_kaneko_infile_known_answer():
+    v = load_vectors(os.path.join(GOLD, "infile_m6t6.txt"))
+    res, l0, st = dec(6, 6).decode(v.y)
+    np.testing.assert_array_equal(res[0], v.res[0])
+    assert l0[0] == v.l0[0]
+    assert st["decodes"][0] == 524287
+    assert (st["comparisons"][0], st["sums"][0]) == (v.cmp[0], v.sums[0])
+
+
+def test_word_variant_infile_known_answer():
+    # decode(word, res) (src/KanekoKernelProcessor.cpp:212): 524288 decodes
+    F = load()
+    v = load_vectors(os.path.join(GOLD, "infile_m6t6.txt"))
+    res, l0, st = dec(6, 6).decode(v.y, variant=F.VARIANT_WORD)
+    np.testing.assert_array_equal(res[0], v.res[0])
+    assert st["decodes"][0] == 524288
+
+
+@pytest.mark.parametrize("m,t,snr,B", [(6, 6, 3.0, 64), (6, 6, 4.0, 256), (6, 6, 5.0, 512),
+                                       (5, 3, 1.0, 256), (4, 2, 0.0, 512), (8, 15, 5.0, 32)])
+def test_kaneko_j15_matches_oracle(m, t, snr, B):
+    o = Oracle(m, t)
+    _, y = o.stream(101, B, snr)
+    res, l0, st = dec(m, t, J=15).decode(y)
+    r2, l2, s2, a2 = o.kaneko_batch(y, J=15)
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, res, l0, st)
+
+
+@pytest.mark.parametrize("path", sweep_files(), ids=os.path.basename)
+def test_gpu_sweep_csv_identical_to_reference(path):
+    name = os.path.basename(path)[len("sweep_"):-4]
+    mt, p, e = name.split("_")
+    m, t = int(mt[1:mt.index("t")]), int(mt[mt.index("t") + 1:])
+    assert dec(m, t).sweep(int(p[1:]), int(e[1:])) == open(path).read()
+
+
+def test_gpu_sweep_j15_bch31_pinned_md5():
+    # reference BCH(31,16,7), J=15, p=1e6, e=100
+    csv = dec(5, 3, J=15).sweep(1000000, 100)
+    assert hashlib.md5(csv.encode()).hexdigest() == "105c77e4bb47a243054121d9c907feae"
+
+
+def test_generator_stream_matches_oracle():
+    o = Oracle(6, 6)
+    tx0, y0 = o.stream(9, 100, 4.5)
+    tx, y, state = dec(6, 6).generate(4.5, 100, seed=9)
+    np.testing.assert_array_equal(tx, tx0)
+    np.testing.assert_array_equal(y.view(np.uint64), y0.view(np.uint64))
+    # continuing from the returned state equals one long call
+    _, ya, st_a = dec(6, 6).generate(4.5, 30, seed=9)
+    _, yb, _ = dec(6, 6).generate(4.5, 70, state=st_a)
+    np.testing.assert_array_equal(np.vstack([ya, yb]).view(np.uint64), y.view(np.uint64))
+
+
+def test_untouched_rows_and_edge_inputs():
+    F = load()
+    d = dec(6, 6)
+    # all-zero channel (every |alpha| tied at 0): flagged as a tie, still terminates
+    y = np.zeros((2, 63))
+    y[1] = np.linspace(-1, 1, 63)  # exact zero at the centre, no ties otherwise
+    d.set_max_decodes(1 << 20)
+    res, l0, st = d.decode(y)
+    assert st["flags"][0] & F.F_TIE
+    d.set_max_decodes(0)
+    # empty batch
+    r, l, s = d.decode(np.zeros((0, 63)))
+    assert r.shape == (0, 63)
+
+
+def test_max_decodes_cap_flags_truncation():
+    F = load()
+    v = load_vectors(os.path.join(GOLD, "infile_m6t6.txt"))
+    d = load().KanekoKernelProcessor(6, 6)
+    d.set_max_decodes(1000)
+    res, l0, st = d.decode(v.y)
+    assert st["flags"][0] & F.F_TRUNCATED
+    assert st["decodes"][0] <= 1024
+
+
+def test_large_batch_sampled_against_oracle_and_deterministic():
+    # full headline batch size: sampled rows vs the oracle, and run-to-run identity
+    o = Oracle(6, 6)
+    d = dec(6, 6, J=15)
+    tx, y, _ = d.generate(5.0, 1 << 18, seed=77)
+    res, l0, st = d.decode(y)
+    res2, l02, st2 = d.decode(y)
+    np.testing.assert_array_equal(res, res2)
+    np.testing.assert_array_equal(l0.view(np.uint64), l02.view(np.uint64))
+    np.testing.assert_array_equal(st, st2)
+    idx = np.random.default_rng(1).choice(len(y), 300, replace=False)
+    r2, l2, s2, a2 = o.kaneko_batch(y[idx], J=15)
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, res[idx], l0[idx], st[idx])
+    # decoded words are codewords or flagged non-ML; FER is plausible for 5 dB (<1e-3)
+    fer = np.mean(np.any(res != tx, axis=1))
+    assert fer < 1e-3
