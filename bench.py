@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Throughput of the Kaneko BCH soft decoder on MI355X (one process per GPU).
+
+A step = one pass of the hot path over one resident batch: Kaneko decode of B codewords
+(libbchk search kernel) + FER/op counter reduction (+ one RCCL all-reduce of the 6
+counters when N > 1). Inputs are the reference's own channel stream (minstd_rand0 +
+libstdc++ distributions, rank-specific seed), generated on the host and resident in HBM
+before timing. Weak scaling: every rank decodes its own B codewords.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line (driver contract) with `roofline` (HIP-event kernel time of
+the search kernel vs the 8 TB/s HBM roof at 9n+8 algorithmic bytes per codeword) and
+`cpu_baseline` (the reference itself, compiled into oracle/_ref, timed on one host core on
+a bounded sample of the same workload).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+METRIC = "codewords/s + FER vs Eb/N0, BCH(63,30,13) L=8 batch=2^20"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--m", type=int, default=6)
+    ap.add_argument("--t", type=int, default=6)
+    ap.add_argument("--snr", type=float, default=5.0, help="Eb/N0 in dB")
+    ap.add_argument("--J", type=int, default=15, help="test-pattern cap; -1 = shipped (uncapped)")
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target CPU time of the cpu_baseline sample (0 = skip)")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def load_pkg():
+    import importlib.util
+    pkg = os.path.join(REPO, "polar-codes-with-bch-kernel_amd")
+    spec = importlib.util.spec_from_file_location("bchk_amd", os.path.join(pkg, "__init__.py"),
+                                                  submodule_search_locations=[pkg])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["bchk_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def cpu_baseline(args, gpu_rate):
+    """The reference decode(answer, word, res) on one host core, same code/SNR/J."""
+    if args.cpu_seconds <= 0:
+        return None
+    exe = os.path.join(REPO, "oracle", "_ref", "ref_golden_j15" if args.J == 15 else "ref_golden")
+    kind = "reference"
+    if args.J not in (15, -1) or not os.path.exists(exe):
+        exe, kind = None, "port"
+    # size the sample from a short probe so the whole leg takes ~cpu_seconds
+    probe = 2000
+    if exe:
+        def run(count):
+            out = subprocess.run([exe, "bench", str(args.m), str(args.t), str(args.seed), str(count),
+                                  repr(args.snr)], capture_output=True, text=True, check=True).stdout
+            return json.loads(out.strip().splitlines()[-1])
+        r = run(probe)
+        count = int(max(probe, min(2_000_000, r["codewords_per_s"] * args.cpu_seconds)))
+        r = run(count)
+        rate, words = r["codewords_per_s"], r["words"]
+    else:
+        from oracle_lib import Oracle
+        o = Oracle(args.m, args.t)
+        _, y = o.stream(args.seed, probe, args.snr)
+        t0 = time.perf_counter()
+        o.kaneko_batch(y, J=args.J)
+        rate = probe / (time.perf_counter() - t0)
+        count = int(max(probe, min(200_000, rate * args.cpu_seconds)))
+        _, y = o.stream(args.seed, count, args.snr)
+        t0 = time.perf_counter()
+        o.kaneko_batch(y, J=args.J)
+        rate, words = count / (time.perf_counter() - t0), count
+    return {"value": round(rate, 3), "unit": "codewords/s", "cores": 1, "kind": kind,
+            "sample": f"first {words} codewords of the reference stream (seed {args.seed}) at "
+                      f"Eb/N0={args.snr} dB, J={'inf' if args.J < 0 else args.J}, BCH("
+                      f"{(1 << args.m) - 1}) t={args.t}; decode calls only, 1 thread",
+            "gpu_over_cpu": round(gpu_rate / rate, 1) if rate > 0 else None}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    bchk = load_pkg()
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dec = bchk.KanekoKernelProcessor(args.m, args.t, J=args.J, device=local)
+    n, B = dec.n, args.batch
+    t_gen = time.perf_counter()
+    tx, y, _ = dec.generate(args.snr, B, seed=args.seed + 7919 * rank)
+    t_gen = time.perf_counter() - t_gen
+    dev = torch.device("cuda", local)
+    d_y = torch.from_numpy(y).to(dev)
+    d_tx = torch.from_numpy(tx).to(dev)
+    d_res = torch.zeros((B, n), dtype=torch.uint8, device=dev)
+    d_l0 = torch.empty(B, dtype=torch.float64, device=dev)
+    d_st = torch.empty((B, bchk.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    d_cnt = torch.zeros(6, dtype=torch.int64, device=dev)
+    stream = torch.cuda.ExternalStream(dec.stream, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        dec.decode_device(d_y.data_ptr(), B, d_res.data_ptr(), d_l0.data_ptr(), d_st.data_ptr(),
+                          dec.stream)
+        dec.count_device(d_tx.data_ptr(), d_res.data_ptr(), d_st.data_ptr(), B, d_cnt.data_ptr(),
+                         dec.stream)
+        if world > 1:
+            with torch.cuda.stream(stream):
+                dist.all_reduce(d_cnt)
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+        dec.sync()
+        d_cnt.zero_()
+        dec.sync()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dec.profile(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        dec.sync()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+    kern_ms, launches = dec.profile_read()
+    dec.profile(False)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    cnt = d_cnt.cpu().numpy().astype(np.int64)  # summed over ranks (N > 1)
+    total_words = world * B * args.steps
+    value = total_words / elapsed
+    kernel_s = kern_ms / 1e3 / max(1, launches)
+    bytes_per_cw = 9 * n + 8  # 8n B f64 samples in + n B decoded bits + 8 B l0 out
+    achieved = bytes_per_cw * B / kernel_s / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tr = json.load(open(args.traffic))
+            if tr.get("batch") == B and tr.get("snr_db") == args.snr and tr.get("J") == args.J:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if rank == 0:
+        words = int(cnt[5])
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "codewords/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: the reference's AWGN stream (minstd_rand0 + libstdc++ "
+                    "distributions), BPSK, generated on host, resident in HBM",
+            "config": {"workload": f"Kaneko ML soft decoding of BCH({n},{dec.k},{2 * args.t + 1}), "
+                                   f"Eb/N0={args.snr} dB, J={'inf' if args.J < 0 else args.J}",
+                       "code": f"BCH({n},{dec.k},{2 * args.t + 1})", "batch_per_gpu": B,
+                       "global_batch": world * B, "snr_db": args.snr, "J": args.J,
+                       "L": 8, "parallelism": f"dp{world}"},
+            "fer": (int(cnt[0]) / words) if words else None,
+            "ber": (int(cnt[1]) / words / n) if words else None,
+            "decodes_per_codeword": (int(cnt[2]) / words) if words else None,
+            "kernel_ms": round(kernel_s * 1e3, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": traffic},
+            "host_generation_s": round(t_gen, 2),
+        }
+        if world == 1:
+            out["cpu_baseline"] = cpu_baseline(args, value)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
