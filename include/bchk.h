@@ -117,17 +117,26 @@ int bchk_generate_host(const bchk_ctx *ctx, double snr_db, size_t B, uint64_t *r
 
 /* fun(file, decoder, g, gSize, p, e, maxSTNR) (headers/dataForPlot.h:8,
  * src/dataForPlot.cpp:16-116) on the GPU: identical CSV text, written to csv (cap bytes,
- * NUL-terminated). batch = codewords decoded per GPU launch (0 = auto). */
-int bchk_sweep(bchk_ctx *ctx, long p, long e, double max_snr, uint64_t seed, size_t batch,
-               char *csv, size_t cap);
+ * NUL-terminated). The stream starts from *rng_state (engine state; NULL or 0 = seed) and
+ * *rng_state receives the state after the last word consumed, exactly where the
+ * reference's global engine would be. batch = codewords per GPU launch (0 = auto). */
+int bchk_sweep(bchk_ctx *ctx, long p, long e, double max_snr, uint64_t *rng_state,
+               uint64_t seed, size_t batch, char *csv, size_t cap);
 
 int bchk_sync(bchk_ctx *ctx);
 /* the context's HIP stream (hipStream_t) */
 void *bchk_stream(bchk_ctx *ctx);
-/* Average duration (ms) of the search kernel over the last *_device calls made with
- * bchk_profile(ctx, 1) enabled (HIP events recorded on the launch stream). */
+/* Kernel-time profiling with HIP events recorded on the launch stream around each
+ * decode call: the lane-per-codeword fast kernel and the exact wave-per-codeword kernel
+ * (which also runs alone when the fast path is off or unavailable). read() returns the
+ * summed milliseconds since the last read and the number of decode calls, then resets. */
 int bchk_profile(bchk_ctx *ctx, int enable);
-int bchk_profile_read(bchk_ctx *ctx, double *total_ms, uint64_t *launches);
+int bchk_profile_read(bchk_ctx *ctx, double *fast_ms, double *slow_ms, uint64_t *launches);
+/* Codewords the last decode call on the context's stream handed from the fast path to
+ * the exact wave-per-codeword kernel (synchronises the context's stream). */
+int bchk_slow_count(bchk_ctx *ctx, uint64_t *count);
+/* Enable (default) or disable the fast path; results are identical either way. */
+int bchk_set_fast_path(bchk_ctx *ctx, int enable);
 const char *bchk_last_error(void);
 const char *bchk_version(void);
 

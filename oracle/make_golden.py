@@ -15,6 +15,8 @@ Fixture formats (gzip text, one record per line):
   infile_m6t6.txt    the in/infile.txt known answer, same 'W' line (counters absolute)
   algdec_*.txt.gz    'A <word bits> <ok> <answer bits | ->'  (src/Decoder.cpp:298)
   sweep_*.csv        the reference CLI `kaneko m t file p e` output (src/dataForPlot.cpp:80)
+  cli_*.txt          stdout of the reference CLI modes 1 and 3 (src/main.cpp:100-172)
+  infile_input.txt   the reference's in/infile.txt fixture (input data of mode 3)
 """
 import gzip
 import os
@@ -64,6 +66,15 @@ def main():
         with gzip.open(os.path.join(GOLD, name), "wt") as f:
             f.write(out)
         print(name, len(out))
+    # CLI modes 1 and 3 of src/main.cpp (stdout), and the mode-3 input itself (data)
+    for args, name in ((["6", "6", "0.0", "/root/reference/in/infile.txt"], "cli_infile_m6t6.txt"),
+                       (["6", "6", "3.0"], "cli_random_m6t6_snr3.txt"),
+                       (["4", "2", "4.0"], "cli_random_m4t2_snr4.txt")):
+        with open(os.path.join(GOLD, name), "w") as f:
+            f.write(run([os.path.join(REF, "kaneko")] + args))
+    with open("/root/reference/in/infile.txt") as src, \
+            open(os.path.join(GOLD, "infile_input.txt"), "w") as dst:
+        dst.write(src.read())
     tmp = os.path.join(REF, "sweep_tmp")
     os.makedirs(tmp, exist_ok=True)
     for m, t, p, e in SWEEPS:

@@ -31,7 +31,7 @@ EXPORTS = (
     "bchk_set_max_decodes", "bchk_decode_host", "bchk_decode_device",
     "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device",
     "bchk_generate_host", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
-    "bchk_profile_read", "bchk_last_error", "bchk_version",
+    "bchk_profile_read", "bchk_slow_count", "bchk_set_fast_path", "bchk_last_error", "bchk_version",
 )
 
 STATS_DTYPE = np.dtype([("decodes", "<u8"), ("comparisons", "<u8"), ("sums", "<u8"),
@@ -81,12 +81,14 @@ def lib():
     L.bchk_alg_decode_host.argtypes = [vp, vp, vp, sz, vp, vp]
     L.bchk_count_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
     L.bchk_generate_host.argtypes = [vp, dbl, sz, C.POINTER(u64), u64, vp, vp]
-    L.bchk_sweep.argtypes = [vp, C.c_long, C.c_long, dbl, u64, sz, C.c_char_p, sz]
+    L.bchk_sweep.argtypes = [vp, C.c_long, C.c_long, dbl, C.POINTER(u64), u64, sz, C.c_char_p, sz]
     L.bchk_sync.argtypes = [vp]
     L.bchk_stream.argtypes = [vp]
     L.bchk_stream.restype = vp
     L.bchk_profile.argtypes = [vp, i32]
-    L.bchk_profile_read.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
+    L.bchk_profile_read.argtypes = [vp, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(u64)]
+    L.bchk_set_fast_path.argtypes = [vp, i32]
+    L.bchk_slow_count.argtypes = [vp, C.POINTER(u64)]
     L.bchk_last_error.restype = C.c_char_p
     L.bchk_version.restype = C.c_char_p
     _lib = L
@@ -175,11 +177,12 @@ class KanekoKernelProcessor:
         _check(lib().bchk_generate_host(self._h, snr_db, B, C.byref(st), seed, _p(tx), _p(y)))
         return tx, y, st.value
 
-    def sweep(self, p, e, max_snr=5.0, seed=1, batch=0):
-        """fun() on the GPU: the reference CSV text."""
+    def sweep(self, p, e, max_snr=5.0, seed=1, batch=0, state=0, return_state=False):
+        """fun() on the GPU: the reference CSV text (and the engine state after it)."""
         buf = C.create_string_buffer(1 << 16)
-        _check(lib().bchk_sweep(self._h, p, e, max_snr, seed, batch, buf, len(buf)))
-        return buf.value.decode()
+        st = C.c_uint64(state)
+        _check(lib().bchk_sweep(self._h, p, e, max_snr, C.byref(st), seed, batch, buf, len(buf)))
+        return (buf.value.decode(), st.value) if return_state else buf.value.decode()
 
     def sync(self):
         _check(lib().bchk_sync(self._h))
@@ -192,9 +195,19 @@ class KanekoKernelProcessor:
         _check(lib().bchk_profile(self._h, 1 if enable else 0))
 
     def profile_read(self):
-        ms, n = C.c_double(), C.c_uint64()
-        _check(lib().bchk_profile_read(self._h, C.byref(ms), C.byref(n)))
-        return ms.value, n.value
+        """(fast-kernel ms, slow-kernel ms, decode calls) since the last read."""
+        a, b, n = C.c_double(), C.c_double(), C.c_uint64()
+        _check(lib().bchk_profile_read(self._h, C.byref(a), C.byref(b), C.byref(n)))
+        return a.value, b.value, n.value
+
+    def slow_count(self):
+        """Codewords the last decode handed to the exact wave-per-codeword kernel."""
+        n = C.c_uint64()
+        _check(lib().bchk_slow_count(self._h, C.byref(n)))
+        return n.value
+
+    def set_fast_path(self, enable=True):
+        _check(lib().bchk_set_fast_path(self._h, 1 if enable else 0))
 
 
 def version():

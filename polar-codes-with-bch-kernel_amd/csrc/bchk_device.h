@@ -36,6 +36,14 @@ struct SearchParams {
     double s2;             // pow(sd0, 2), host glibc (src/KanekoKernelProcessor.cpp:337)
     uint64_t max_decodes;  // 0 = unlimited
     uint32_t count;        // codewords
+    // slow-path work queue (null = process codewords [0, count) in place):
+    //   queue[0 .. *qcount) codeword indices, dequeued through 8 per-XCD heads
+    //   heads[32 * x] (one 128-B line each), zeroed before the launch.
+    const uint32_t *queue;
+    const uint32_t *qcount;
+    uint32_t *heads;
+    uint32_t *qtail;       // fast path: append unresolved codewords here (with queue_out)
+    uint32_t *queue_out;
     int32_t t;
     int32_t J;             // < 0: shipped
     int32_t variant;       // BCHK_VARIANT_*

@@ -1,0 +1,265 @@
+// bchk_fast.hip -- lane-per-codeword fast path of the Kaneko search (n <= 63).
+//
+// At the SNRs where the decoder is used, most codewords leave the reference loop
+// (src/KanekoKernelProcessor.cpp:361-405) through `l < calcRightSide()` at test pattern
+// i = 0 (the hard decision lies within t of a codeword) or i = 1 (the hard decision is a
+// codeword: its zero syndrome fails, flipping the least reliable bit succeeds). This kernel
+// gives every lane its own codeword and decides exactly those two cases:
+//   - the row is staged through LDS in 8-position slices (coalesced 8-B loads), each lane
+//     builds 32-bit sort keys (26-bit monotone prefix of |y|, 6-bit position) and sorts
+//     them with a 64-key bitonic network in registers;
+//   - distinct prefixes order alpha = |2y/s2| exactly; a prefix tie within the sorted
+//     prefix calcRightSide can touch (3t+3 entries) sends the codeword to the exact slow
+//     path; the alphas that enter sums are recomputed exactly (IEEE f64 division of the
+//     row's samples, gathered on demand);
+//   - decodes i = 0 and i = 1 run per lane (binary BM + Chien table);
+//   - calcL / calcRightSide are summed in the reference's order.
+// Codewords not resolved here (no early return at i <= 1, or any doubt) are appended to a
+// queue that the wave-per-codeword kernel (bchk_kernels.hip) processes from scratch, so
+// every result is the reference's.
+#include "bchk_core.h"
+#include "bchk_launch.h"
+
+namespace bchk {
+
+namespace {
+constexpr int kRowD = 9;  // doubles per staged row slice (8 + 1 pad: conflict-free b64)
+constexpr int kSlice = 8;
+}  // namespace
+
+// 32-bit sort key: a monotone 26-bit prefix of |y| (5 exponent bits covering
+// [2^-27, 2^5) + 21 mantissa bits) above the 6-bit position. |y| below the range maps to
+// prefix 0, above it (and inf/NaN) to the all-ones prefix; both are detected after the sort.
+__device__ __forceinline__ uint32_t sort_key(uint32_t hi, uint32_t lo, int pos) {
+    const uint32_t ahi = hi & 0x7FFFFFFFu;
+    const int eb = (int)(ahi >> 20) - (1023 - 27);
+    const uint32_t mant21 = ((ahi & 0xFFFFFu) << 1) | (lo >> 31);
+    const uint32_t mid = ((uint32_t)eb << 21) | mant21;
+    const uint32_t pre = eb < 0 ? 0u : (eb > 31 ? 0x3FFFFFFu : mid);
+    return (pre << 6) | (uint32_t)pos;
+}
+
+template <int M, int TMAX>
+__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock)
+kaneko_fast_kernel(SearchParams p) {
+    constexpr int N = Geo<M>::N;
+    static_assert(N <= 63, "fast path covers n <= 63");
+    constexpr int W = (TMAX + 3) / 4;
+    constexpr int KMAX = (3 * TMAX + 2 < N - 1) ? 3 * TMAX + 2 : N - 1;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    load_tables(smem, p.tables, p.td.bytes);
+    __syncthreads();
+    const uint8_t *ex = smem + p.td.off_exp;
+    const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
+    const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
+    const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double *stage = reinterpret_cast<double *>(smem + ((p.td.bytes + 15) & ~15u) +
+                                               wid * (64 * kRowD * 8));
+    const uint32_t cw0 = (blockIdx.x * kWavesPerBlock + wid) * 64u;
+    if (cw0 >= p.count) return;
+    const uint32_t cw = cw0 + (uint32_t)lane;
+    const bool live = cw < p.count;
+    const int t = p.t;
+    (void)M;
+    const double s2 = p.s2;
+    const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
+
+    // ---- stage rows, build keys and the hard decision yH = (2y/s2 > 0) (:336-342)
+    const uint32_t last_row = p.count - 1u - cw0;  // rows past the batch end clamp (unused)
+    uint32_t key[64];
+    uint64_t yH = 0;
+#pragma unroll
+    for (int c = 0; c < (N + kSlice - 1) / kSlice; ++c) {
+        double v[kSlice];
+#pragma unroll
+        for (int it = 0; it < kSlice; ++it) {
+            const int flat = it * 64 + lane;
+            const uint32_t r = (uint32_t)(flat >> 3);
+            const int pos = kSlice * c + (flat & 7);
+            const uint32_t rr = r < last_row ? r : last_row;
+            v[it] = p.y[(size_t)(cw0 + rr) * N + (pos < N ? pos : N - 1)];
+        }
+#pragma unroll
+        for (int it = 0; it < kSlice; ++it) {
+            const int flat = it * 64 + lane;
+            stage[(flat >> 3) * kRowD + (flat & 7)] = v[it];
+        }
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < kSlice; ++k) {
+            const int pos = kSlice * c + k;
+            if (pos < N) {
+                const uint64_t b = (uint64_t)__double_as_longlong(stage[lane * kRowD + k]);
+                const uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
+                key[pos] = sort_key(hi, lo, pos);
+                // y > 0 (sign clear, nonzero); tiny/subnormal y, whose alpha could underflow,
+                // has prefix 0 and is sent to the slow path below
+                yH |= (uint64_t)(((int32_t)hi >= 0) && ((hi | lo) != 0u)) << pos;
+            }
+        }
+        wave_sync();
+    }
+#pragma unroll
+    for (int q = N; q < 64; ++q) key[q] = 0xFFFFFFFFu;
+
+    // ---- bitonic sort of the 64 keys, ascending
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint32_t a = key[i], b = key[l];
+                    const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+                    key[i] = (i & k) ? hi : lo;
+                    key[l] = (i & k) ? lo : hi;
+                }
+            }
+        }
+    }
+
+    // ---- sorted prefix. Distinct 26-bit prefixes imply |y| values >= 2^-21 apart
+    // (relative), so their alphas are strictly ordered exactly as the reference's
+    // (|alpha|, position) order; any equal prefix up to the boundary pair (KMAX, KMAX+1)
+    // sends the codeword to the exact slow path.
+    bool bad = (key[0] >> 6) == 0u                       // some |y| < 2^-27 (or zero)
+               || (key[N - 1] >> 6) == 0x3FFFFFFu;       // some |y| >= 32, inf or NaN
+#pragma unroll
+    for (int r = 0; r <= KMAX && r < 63; ++r) bad |= ((key[r] ^ key[r + 1]) >> 6) == 0u;
+    auto alpha_at = [&](int pos) { return fabs((2.0 * yrow[pos]) / s2); };
+
+    // ---- syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
+    uint32_t S0[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) S0[w] = 0;
+#pragma unroll
+    for (int pos = 0; pos < N; ++pos) {
+        const uint32_t on = ((yH >> pos) & 1ull) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+        for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w] & on;
+    }
+
+    // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`.
+    auto accept = [&](uint64_t diff, double &l, bool &ret) {
+        const int m = __popcll(diff);
+        const int border = (2 * t + 1) - m;  // m0 == m on both fast-path exits
+        l = 0.0;
+        for (uint64_t v = diff; v; v &= v - 1) l += alpha_at(__builtin_ctzll(v));
+        double rs = 0.0;
+        int taken = 0;
+#pragma unroll
+        for (int r = 0; r <= KMAX; ++r) {
+            const int o = (int)(key[r] & 63u);
+            const bool ag = !((diff >> o) & 1ull);
+            if (ag && taken < border) {
+                rs += alpha_at(o);
+                ++taken;
+            }
+        }
+        ret = (taken >= border) && (l < rs);  // otherwise: ran past the exact prefix / no return
+    };
+
+    // ---- i = 0 (:361-382)
+    int state = 0;  // 0 unresolved, 1 returned at i = 0, 2 returned at i = 1
+    uint64_t best = 0;
+    double l0 = DBL_MAX;
+    Mask<1> E;
+    const bool ok0 = alg_core<M, TMAX>(ex, lg, chien, S0, t, E);
+    if (!bad && ok0) {
+        double l;
+        bool ret;
+        accept(E.w[0], l, ret);
+        if (ret) { state = 1; best = E.w[0]; l0 = l; }
+    }
+    // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371)
+    const bool need1 = live && !bad && !ok0;
+    if (ballot(need1)) {
+        const int o0 = (int)(key[0] & 63u);
+        uint32_t S1[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) S1[w] = S0[w] ^ col[o0 * W + w];
+        const bool ok1 = alg_core<M, TMAX>(ex, lg, chien, S1, t, E);
+        if (need1 && ok1) {
+            const uint64_t diff = (1ull << o0) ^ E.w[0];
+            double l;
+            bool ret;
+            accept(diff, l, ret);
+            if (ret) { state = 2; best = diff; l0 = l; }
+        }
+    }
+
+    // ---- outputs: resolved rows through LDS, one coalesced 64-row block per wave
+    const bool resolved = live && state != 0;
+    uint8_t *out = reinterpret_cast<uint8_t *>(stage);
+    const uint64_t x = yH ^ best;
+    if (resolved) {
+#pragma unroll
+        for (int pos = 0; pos < N; ++pos) out[lane * N + pos] = (uint8_t)((x >> pos) & 1ull);
+    } else if (live) {  // unresolved: keep the caller's row as it is
+        for (int pos = 0; pos < N; ++pos) out[lane * N + pos] = p.res[(size_t)cw * N + pos];
+    }
+    wave_sync();
+    uint8_t *dst = p.res + (size_t)cw0 * N;
+    if (cw0 + 64u <= p.count && ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0)) {
+        const uint4 *src4 = reinterpret_cast<const uint4 *>(out);
+        uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
+        for (int i = lane; i < 4 * N; i += 64) dst4[i] = src4[i];
+    } else {
+        const int rows = (int)((p.count - cw0) < 64u ? (p.count - cw0) : 64u);
+        for (int i = lane; i < rows * N; i += 64) dst[i] = out[i];
+    }
+    if (resolved) {
+        const bool word = p.variant == BCHK_VARIANT_WORD;
+        const uint64_t pro = word ? (uint64_t)(2 * N + 1) : 0ull;
+        const uint64_t iters = state == 2 ? 1ull : 0ull;
+        if (p.l0) p.l0[cw] = l0;
+        if (p.st) {
+            bchk_stats st;
+            st.decodes = iters + 1;
+            st.comparisons = pro + iters * (uint64_t)(N + 6);
+            st.sums = pro + iters * (uint64_t)(N + 1);
+            st.iterations = iters;
+            st.jsteps = 0;
+            st.improvements = 0;
+            st.flags = BCHK_F_ACCEPTED | BCHK_F_RETURNED;
+            st.reserved = 0;
+            p.st[cw] = st;
+        }
+    }
+    // ---- everything else goes to the exact wave-per-codeword path
+    const bool unres = live && state == 0;
+    const uint64_t um = ballot(unres);
+    if (um) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(p.qtail, (uint32_t)__popcll(um));
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        if (unres) p.queue_out[base + (uint32_t)__popcll(um & ((1ull << lane) - 1ull))] = cw;
+    }
+}
+
+template <int M, int TMAX>
+static hipError_t launch_fast_impl(const SearchParams &p, size_t lds, hipStream_t s) {
+    const int blocks = (int)((p.count + 255u) / 256u);
+    hipLaunchKernelGGL((kaneko_fast_kernel<M, TMAX>), dim3(blocks), dim3(kWaveSize * kWavesPerBlock),
+                       lds, s, p);
+    return hipGetLastError();
+}
+
+size_t fast_wave_bytes() { return (size_t)64 * kRowD * 8; }
+
+// Fast-path instantiations (n <= 63, small t): (m, TMAX) as in select_kernels.
+bool select_fast(int m, int t, FastFn *out) {
+#define BCHK_FAST(MM, TT) \
+    if (m == MM && t <= TT) { *out = &launch_fast_impl<MM, TT>; return true; }
+    BCHK_FAST(3, 3)
+    BCHK_FAST(4, 2) BCHK_FAST(4, 7)
+    BCHK_FAST(5, 3) BCHK_FAST(5, 8)
+    BCHK_FAST(6, 6)
+#undef BCHK_FAST
+    return false;
+}
+
+}  // namespace bchk

@@ -12,6 +12,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -182,6 +183,10 @@ struct bchk_ctx {
     std::vector<uint8_t> tables_host;
     TableDesc td{};
     KernelSet ks{};
+    FastFn fast = nullptr;
+    bool use_fast = true;
+    size_t lds_fast = 0;
+    DevBuf queue, ctrl;  // slow-path work queue + {tail, 8 per-XCD heads} (128-B lines)
     uint8_t *d_tables = nullptr;
     hipStream_t stream = nullptr;
     size_t lds = 0, lds_alg = 0;
@@ -189,8 +194,9 @@ struct bchk_ctx {
     uint64_t max_decodes = 0;
     DevBuf y, res, l0, st, words, synd, ok;
     bool profile = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
-    double prof_ms = 0.0;
+    struct Ev { hipEvent_t a, b, c; };
+    std::vector<Ev> events;
+    double prof_fast_ms = 0.0, prof_slow_ms = 0.0;
     uint64_t prof_launches = 0;
 };
 
@@ -202,6 +208,8 @@ int sigma_s2(int k, int n, double snr_db, double *sd) {
     *sd = sqrt(1 / (pow(10, snr_db / 10) * 2 * K / Nn));
     return 0;
 }
+
+constexpr size_t kCtrlBytes = 9 * 128;  // tail at word 0, head x at word 32 (x + 1)
 
 int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t *d_res,
                   double *d_l0, bchk_stats *d_st, hipStream_t s) {
@@ -220,18 +228,39 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     p.t = c->t;
     p.J = c->J;
     p.variant = variant;
-    const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
-    const int grid = std::max(1, std::min(c->grid, need));
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (c->profile) {
         HIP_TRY(hipEventCreate(&e0));
         HIP_TRY(hipEventCreate(&e1));
+        HIP_TRY(hipEventCreate(&e2));
         HIP_TRY(hipEventRecord(e0, s));
     }
-    HIP_TRY(launch_search(c->ks, p, grid, c->lds, s));
+    if (c->fast && c->use_fast) {
+        int rc;
+        if ((rc = c->queue.ensure(B * sizeof(uint32_t))) || (rc = c->ctrl.ensure(kCtrlBytes))) return rc;
+        uint32_t *ctrl = (uint32_t *)c->ctrl.p;
+        HIP_TRY(hipMemsetAsync(ctrl, 0, kCtrlBytes, s));
+        p.qtail = ctrl;
+        p.queue_out = (uint32_t *)c->queue.p;
+        HIP_TRY(c->fast(p, c->lds_fast, s));
+        if (c->profile) HIP_TRY(hipEventRecord(e1, s));
+        SearchParams q = p;
+        q.queue = (const uint32_t *)c->queue.p;
+        q.qcount = ctrl;
+        q.heads = ctrl + 32;
+        q.qtail = nullptr;
+        q.queue_out = nullptr;
+        // every resident wave may take work; waves beyond the queue length exit at once
+        HIP_TRY(launch_search(c->ks, q, c->grid, c->lds, s));
+    } else {
+        const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
+        const int grid = std::max(1, std::min(c->grid, need));
+        if (c->profile) HIP_TRY(hipEventRecord(e1, s));
+        HIP_TRY(launch_search(c->ks, p, grid, c->lds, s));
+    }
     if (c->profile) {
-        HIP_TRY(hipEventRecord(e1, s));
-        c->events.emplace_back(e0, e1);
+        HIP_TRY(hipEventRecord(e2, s));
+        c->events.push_back({e0, e1, e2});
     }
     return 0;
 }
@@ -287,6 +316,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     const size_t tb = (c->td.bytes + 15) & ~size_t(15);
     c->lds = tb + kWavesPerBlock * c->ks.wave_bytes;
     c->lds_alg = tb;
+    if (select_fast(m, t, &c->fast)) c->lds_fast = tb + kWavesPerBlock * fast_wave_bytes();
+    if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     const void *fn = c->ks.search_ptr();
     if (c->lds > 65536)
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
@@ -305,9 +336,12 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
 void bchk_destroy(bchk_ctx *c) {
     if (!c) return;
     for (auto &e : c->events) {
-        hipEventDestroy(e.first);
-        hipEventDestroy(e.second);
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+        (void)hipEventDestroy(e.c);
     }
+    c->queue.release();
+    c->ctrl.release();
     c->y.release();
     c->res.release();
     c->l0.release();
@@ -463,13 +497,18 @@ int bchk_generate_host(const bchk_ctx *c, double snr_db, size_t B, uint64_t *rng
     return 0;
 }
 
-int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t seed, size_t batch, char *csv,
-               size_t cap) {
+int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t *rng_state, uint64_t seed,
+               size_t batch, char *csv, size_t cap) {
     if (!c || !csv || cap == 0) return fail(BCHK_EINVAL, "NULL argument");
     if (p <= 0 || e <= 0) return fail(BCHK_EINVAL, "p and e must be positive");
     const size_t n = c->n;
     const size_t max_batch = batch ? batch : (size_t(1) << 18);
     std::default_random_engine eng(seed);
+    if (rng_state && *rng_state) {
+        std::stringstream ss;
+        ss << *rng_state;
+        ss >> eng;
+    }
     std::vector<uint8_t> info(c->k), tx, res, dec(n, 0);
     std::vector<double> y;
     std::vector<bchk_stats> st;
@@ -524,6 +563,11 @@ int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t seed, size_
         wordCount = 0;
         count = 0, countErr = 0;
     }
+    if (rng_state) {
+        std::stringstream ss;
+        ss << eng;
+        ss >> *rng_state;
+    }
     const std::string s = out.str();
     if (s.size() + 1 > cap) return fail(BCHK_EINVAL, "csv buffer too small (%zu needed)", s.size() + 1);
     memcpy(csv, s.c_str(), s.size() + 1);
@@ -536,22 +580,43 @@ int bchk_profile(bchk_ctx *c, int enable) {
     return 0;
 }
 
-int bchk_profile_read(bchk_ctx *c, double *total_ms, uint64_t *launches) {
+int bchk_profile_read(bchk_ctx *c, double *fast_ms, double *slow_ms, uint64_t *launches) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
     for (auto &e : c->events) {
-        HIP_TRY(hipEventSynchronize(e.second));
-        float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second));
-        c->prof_ms += ms;
+        HIP_TRY(hipEventSynchronize(e.c));
+        float a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, e.a, e.b));
+        HIP_TRY(hipEventElapsedTime(&b, e.b, e.c));
+        c->prof_fast_ms += a;
+        c->prof_slow_ms += b;
         c->prof_launches += 1;
-        hipEventDestroy(e.first);
-        hipEventDestroy(e.second);
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+        (void)hipEventDestroy(e.c);
     }
     c->events.clear();
-    if (total_ms) *total_ms = c->prof_ms;
+    if (fast_ms) *fast_ms = c->prof_fast_ms;
+    if (slow_ms) *slow_ms = c->prof_slow_ms;
     if (launches) *launches = c->prof_launches;
-    c->prof_ms = 0.0;
+    c->prof_fast_ms = c->prof_slow_ms = 0.0;
     c->prof_launches = 0;
+    return 0;
+}
+
+int bchk_slow_count(bchk_ctx *c, uint64_t *count) {
+    if (!c || !count) return fail(BCHK_EINVAL, "NULL argument");
+    *count = 0;
+    if (!c->ctrl.p) return 0;
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpyAsync(&v, c->ctrl.p, sizeof v, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *count = v;
+    return 0;
+}
+
+int bchk_set_fast_path(bchk_ctx *c, int enable) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    c->use_fast = enable != 0;
     return 0;
 }
 

@@ -23,174 +23,10 @@
 #include <float.h>
 #include <stdint.h>
 
-#include "bchk_device.h"
+#include "bchk_core.h"
 #include "bchk_launch.h"
 
 namespace bchk {
-
-template <int M>
-struct Geo {
-    static constexpr int N = (1 << M) - 1;
-    static constexpr int NW = (N + 63) / 64;    // u64 words per position mask
-    static constexpr int ZL = 2 * N - 1;        // log(0) sentinel
-    static constexpr int EW = (M + 1) & ~1;     // Chien row u64 words (16-B aligned)
-};
-
-template <int NW>
-struct Mask {
-    uint64_t w[NW];
-};
-
-// ---------------------------------------------------------------- wave helpers
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
-__device__ __forceinline__ uint32_t rdl(uint32_t v, int l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
-__device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
-    return ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32) | rdl((uint32_t)v, l);
-}
-__device__ __forceinline__ double rdlf(double v, int l) {
-    return __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(v), l));
-}
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-// LDS written by some lanes of a wave and read by other lanes of the same wave: DS
-// instructions of one wave execute in order; the fences stop the compiler reordering.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
-    return v;
-}
-
-template <int NW>
-__device__ __forceinline__ void mask_set(Mask<NW> &m, int p) {
-#pragma unroll
-    for (int s = 0; s < NW; ++s)
-        if (s == (p >> 6)) m.w[s] |= 1ull << (p & 63);
-}
-template <int NW>
-__device__ __forceinline__ int mask_popc(const Mask<NW> &m) {
-    int c = 0;
-#pragma unroll
-    for (int s = 0; s < NW; ++s) c += __popcll(m.w[s]);
-    return c;
-}
-
-// ------------------------------------------------------------ algebraic decode
-// Decoder::decode (src/Decoder.cpp:298-321) for one test word, from its packed odd
-// syndromes Sw (byte j = S_{2j+1}). Success iff the syndrome is nonzero, the BM register
-// length L <= t and the locator has deg C >= 1 distinct roots in GF(2^m)*; E = flipped
-// positions ((n - k) mod n for each root alpha^k, :287).
-template <int M, int TMAX>
-__device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
-                                         const uint16_t *__restrict__ lg,
-                                         const uint64_t *__restrict__ chien,
-                                         const uint32_t *Sw, int t,
-                                         Mask<Geo<M>::NW> &E) {
-    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL, NW = Geo<M>::NW;
-    int lS[2 * TMAX];  // lS[j-1] = log S_j
-#pragma unroll
-    for (int j = 0; j < TMAX; ++j) lS[2 * j] = lg[(Sw[j >> 2] >> (8 * (j & 3))) & 0xFFu];
-#pragma unroll
-    for (int e = 2; e <= 2 * TMAX - 1; e += 2) {  // S_{2i} = S_i^2
-        const int h = lS[e / 2 - 1];
-        int sq = 2 * h;
-        sq = sq >= N ? sq - N : sq;
-        lS[e - 1] = (h == ZL) ? ZL : sq;
-    }
-    // inversionless binary Berlekamp-Massey over S_1, S_3, ... (even steps vanish)
-    uint32_t C[TMAX + 1];
-    int lB[TMAX + 1];
-#pragma unroll
-    for (int i = 0; i <= TMAX; ++i) { C[i] = i ? 0u : 1u; lB[i] = i ? ZL : 0; }
-    int lgam = 0, L = 0;
-#pragma unroll
-    for (int k = 0; k < TMAX; ++k) {
-        if (k < t) {
-            const int r = 2 * k;
-            int lC[TMAX + 1];
-#pragma unroll
-            for (int i = 0; i <= TMAX; ++i) lC[i] = lg[C[i]];
-            uint32_t d = 0;
-#pragma unroll
-            for (int i = 0; i <= (r < TMAX ? r : TMAX); ++i) d ^= ex[lC[i] + lS[r - i]];
-            const int ld = lg[d];
-            const bool chg = (d != 0u) && (2 * L <= r);
-#pragma unroll
-            for (int i = TMAX; i >= 0; --i) {
-                const uint32_t g = ex[lgam + lC[i]];
-                C[i] = i ? (g ^ ex[ld + lB[i - 1]]) : g;
-            }
-            // B <- C_old (length change) or x*B; then x*B for the skipped odd step
-#pragma unroll
-            for (int i = TMAX; i >= 0; --i) {
-                const int shifted1 = i ? lB[i - 1] : ZL;
-                const int next = chg ? lC[i] : shifted1;
-                lB[i] = next;
-            }
-#pragma unroll
-            for (int i = TMAX; i >= 1; --i) lB[i] = lB[i - 1];
-            lB[0] = ZL;
-            L = chg ? r + 1 - L : L;
-            lgam = chg ? ld : lgam;
-        }
-    }
-    int deg = 0;
-#pragma unroll
-    for (int i = 1; i <= TMAX; ++i) deg = C[i] ? i : deg;
-    bool ok = (L <= t) && (deg >= 1);
-
-    if constexpr (M <= 6) {
-        constexpr int EW = Geo<M>::EW;
-        uint64_t pl[EW];
-#pragma unroll
-        for (int w = 0; w < EW; ++w) pl[w] = 0;
-#pragma unroll
-        for (int j = 0; j <= TMAX; ++j) {
-            if (j <= t) {
-                const uint64_t *row = chien + (size_t)((j << M) + (int)C[j]) * EW;
-#pragma unroll
-                for (int w = 0; w < EW; ++w) pl[w] ^= row[w];
-            }
-        }
-        uint64_t any = 0;
-#pragma unroll
-        for (int b = 0; b < M; ++b) any |= pl[b];
-        const uint64_t zero = ~any & ((1ull << N) - 1ull);
-        ok = ok && (__popcll(zero) == deg);
-        uint64_t e = __builtin_bitreverse64(zero) >> (63 - N);  // root k -> bit n - k
-        if ((e >> N) & 1ull) e = (e & ((1ull << N) - 1ull)) | 1ull;  // k = 0 -> position 0
-        E.w[0] = e;
-    } else {
-        int lt[TMAX + 1];
-#pragma unroll
-        for (int i = 0; i <= TMAX; ++i) lt[i] = lg[C[i]];
-#pragma unroll
-        for (int s = 0; s < NW; ++s) E.w[s] = 0;
-        int cnt = 0;
-        for (int k = 0; k < N; ++k) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int i = 0; i <= TMAX; ++i) v ^= ex[lt[i]];
-            if (v == 0u) {
-                ++cnt;
-                mask_set<NW>(E, k ? N - k : 0);
-            }
-#pragma unroll
-            for (int i = 1; i <= TMAX; ++i) {
-                int u = lt[i] + i;
-                u = u >= N ? u - N : u;
-                lt[i] = lt[i] == ZL ? ZL : u;
-            }
-        }
-        ok = ok && (cnt == deg);
-    }
-    return ok;
-}
 
 // -------------------------------------------------------------- LDS layout
 template <int M, int TMAX>
@@ -198,13 +34,6 @@ struct Smem {
     static constexpr int NP = 64 * Geo<M>::NW;     // padded positions per wave
     static constexpr int WAVE_BYTES = NP * 8 + NP; // sorted |alpha| (f64) + order (u8)
 };
-
-__device__ __forceinline__ void load_tables(uint8_t *dst, const uint8_t *src, uint32_t bytes) {
-    const uint32_t n16 = bytes / 16;
-    const uint4 *s = reinterpret_cast<const uint4 *>(src);
-    uint4 *d = reinterpret_cast<uint4 *>(dst);
-    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) d[i] = s[i];
-}
 
 // ---------------------------------------------------------- Kaneko search
 // One codeword per wave. Reference: KanekoKernelProcessor::decode(answer, word, res)
@@ -470,9 +299,28 @@ kaneko_search_kernel(SearchParams p) {
     uint8_t *wbase = smem + ((p.td.bytes + 15) & ~15u) + wid * Smem<M, TMAX>::WAVE_BYTES;
     double *as = reinterpret_cast<double *>(wbase);
     uint8_t *ordl = wbase + NP * 8;
-    const uint32_t stride = gridDim.x * kWavesPerBlock;
-    for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride)
-        search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ordl, cw, lane);
+    if (!p.queue) {
+        const uint32_t stride = gridDim.x * kWavesPerBlock;
+        for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride)
+            search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ordl, cw, lane);
+        return;
+    }
+    // Work queue left by the fast path: sub-queue x holds items x, x+8, x+16, ...; a wave
+    // drains its own XCD's sub-queue first (one L2-local atomic per codeword), then steals.
+    const uint32_t total = *p.qcount;
+    int x = xcc_id();
+    for (int exhausted = 0; exhausted < 8;) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(p.heads + 32 * x, 1u);
+        k = (uint32_t)__shfl((int)k, 0, 64);
+        const uint32_t item = (uint32_t)x + 8u * k;
+        if (item >= total) {
+            x = (x + 1) & 7;
+            ++exhausted;
+            continue;
+        }
+        search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ordl, p.queue[item], lane);
+    }
 }
 
 // ------------------------------------------------- batched algebraic decoder

@@ -14,6 +14,12 @@ struct KernelSet {
     size_t wave_bytes;  // LDS bytes per wave of the search kernel
 };
 
+typedef hipError_t (*FastFn)(const SearchParams &, size_t, hipStream_t);
+
+// Lane-per-codeword fast path (bchk_fast.hip); false when (m, t) has none (n > 63, large t).
+bool select_fast(int m, int t, FastFn *out);
+size_t fast_wave_bytes();
+
 // Picks the (m, TMAX) instantiation for runtime t (smallest TMAX >= t).
 bool select_kernels(int m, int t, KernelSet *out);
 hipError_t launch_search(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s);

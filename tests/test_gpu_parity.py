@@ -15,10 +15,12 @@ pytestmark = pytest.mark.gpu
 _ctx = {}
 
 
-def dec(m, t, J=-1):
-    key = (m, t, J)
+def dec(m, t, J=-1, fast=True):
+    key = (m, t, J, fast)
     if key not in _ctx:
-        _ctx[key] = load().KanekoKernelProcessor(m, t, J=J)
+        d = load().KanekoKernelProcessor(m, t, J=J)
+        d.set_fast_path(fast)
+        _ctx[key] = d
     return _ctx[key]
 
 
@@ -65,10 +67,11 @@ def test_alg_decoder_from_stored_syndromes():
     np.testing.assert_array_equal(a1[ok1] ^ words[ok1], a2[ok2])
 
 
+@pytest.mark.parametrize("fast", [True, False], ids=["fast+exact", "exact-only"])
 @pytest.mark.parametrize("path", vector_files(), ids=os.path.basename)
-def test_kaneko_matches_reference_vectors(path):
+def test_kaneko_matches_reference_vectors(path, fast):
     v = load_vectors(path)
-    d = dec(v.m, v.t)
+    d = dec(v.m, v.t, fast=fast)
     assert (d.n, d.k) == (v.n, v.k)
     np.testing.assert_array_equal(d.g, v.g)
     res, l0, st = d.decode(v.y)
@@ -93,12 +96,14 @@ def test_word_variant_infile_known_answer():
     assert st["decodes"][0] == 524288
 
 
+@pytest.mark.parametrize("fast", [True, False], ids=["fast+exact", "exact-only"])
 @pytest.mark.parametrize("m,t,snr,B", [(6, 6, 3.0, 64), (6, 6, 4.0, 256), (6, 6, 5.0, 512),
-                                       (5, 3, 1.0, 256), (4, 2, 0.0, 512), (8, 15, 5.0, 32)])
-def test_kaneko_j15_matches_oracle(m, t, snr, B):
+                                       (6, 6, 6.0, 2048), (5, 3, 1.0, 256), (5, 3, 5.0, 2048),
+                                       (4, 2, 0.0, 512), (4, 2, 6.0, 2048), (8, 15, 5.0, 32)])
+def test_kaneko_j15_matches_oracle(m, t, snr, B, fast):
     o = Oracle(m, t)
     _, y = o.stream(101, B, snr)
-    res, l0, st = dec(m, t, J=15).decode(y)
+    res, l0, st = dec(m, t, J=15, fast=fast).decode(y)
     r2, l2, s2, a2 = o.kaneko_batch(y, J=15)
     check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, res, l0, st)
 
@@ -170,3 +175,37 @@ def test_large_batch_sampled_against_oracle_and_deterministic():
     # decoded words are codewords or flagged non-ML; FER is plausible for 5 dB (<1e-3)
     fer = np.mean(np.any(res != tx, axis=1))
     assert fer < 1e-3
+
+
+def test_fast_path_handles_adversarial_rows():
+    # rows built to hit the fast path's bail-outs: equal |y| (tie), tiny |y|, huge |y|,
+    # exact zeros, a row that is a codeword exactly (+-1); all must equal the oracle.
+    o = Oracle(6, 6)
+    tx, y = o.stream(202, 64, 5.0)
+    y = y.copy()
+    y[0, 5] = -y[0, 9]               # exact |y| tie (flagged, routed to the exact path)
+    y[1, 3] = 1e-12                  # below the key range
+    y[2, 7] = 40.0                   # above the key range
+    y[3, :] = np.where(tx[3] == 1, 1.0, -1.0)  # noiseless codeword: many ties
+    y[4, 11] = 0.0
+    y[5, 0] = np.nextafter(y[5, 1], 0) if y[5, 1] > 0 else y[5, 0]  # near-tie
+    d = dec(6, 6, J=15)
+    d.set_max_decodes(1 << 20)
+    res, l0, st = d.decode(y)
+    d.set_max_decodes(0)
+    F = load()
+    keep = (st["flags"] & (F.F_TIE | F.F_TRUNCATED)) == 0
+    r2, l2, s2, a2 = o.kaneko_batch(y[keep], J=15)
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, res[keep], l0[keep], st[keep])
+    assert st["flags"][0] & F.F_TIE
+
+
+def test_fast_and_exact_paths_agree_at_scale():
+    d_fast, d_exact = dec(6, 6, J=15, fast=True), dec(6, 6, J=15, fast=False)
+    for snr in (4.0, 6.0):
+        _, y, _ = d_fast.generate(snr, 1 << 16, seed=31)
+        a = d_fast.decode(y)
+        b = d_exact.decode(y)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+        np.testing.assert_array_equal(a[2], b[2])
