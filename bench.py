@@ -62,6 +62,27 @@ def dec_tmax(t):
     return t if t in (1, 2, 3, 6, 15) else next(b for b in (7, 8, 12, 16, 31, 32) if b >= t)
 
 
+def rank_seed(seed, rank):
+    """Disjoint per-rank input streams: rank r decodes the stream seeded seed + 7919 r."""
+    return seed + 7919 * rank
+
+
+def reduce_step(step_cnt, total_cnt, world, dist):
+    """One FER exchange per step: the 6 counters of this step are summed over ranks (RCCL
+    all-reduce over xGMI for the nccl backend; gloo on CPU in tests) and accumulated."""
+    if world > 1:
+        dist.all_reduce(step_cnt)
+    total_cnt += step_cnt
+
+
+def max_over_ranks(value, world, dist, device):
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def cpu_baseline(args, gpu_rate):
     """The reference decode(answer, word, res) on one host core, same code/SNR/J."""
     if args.cpu_seconds <= 0:
@@ -116,7 +137,7 @@ def main():
     dec = bchk.KanekoKernelProcessor(args.m, args.t, J=args.J, device=local)
     n, B = dec.n, args.batch
     t_gen = time.perf_counter()
-    tx, y, _ = dec.generate(args.snr, B, seed=args.seed + 7919 * rank)
+    tx, y, _ = dec.generate(args.snr, B, seed=rank_seed(args.seed, rank))
     t_gen = time.perf_counter() - t_gen
     dev = torch.device("cuda", local)
     d_y = torch.from_numpy(y).to(dev)
@@ -124,18 +145,19 @@ def main():
     d_res = torch.zeros((B, n), dtype=torch.uint8, device=dev)
     d_l0 = torch.empty(B, dtype=torch.float64, device=dev)
     d_st = torch.empty((B, bchk.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    d_step = torch.zeros(6, dtype=torch.int64, device=dev)
     d_cnt = torch.zeros(6, dtype=torch.int64, device=dev)
     stream = torch.cuda.ExternalStream(dec.stream, device=dev)
     torch.cuda.synchronize()
 
     def step():
+        # everything below is enqueued on the decoder's stream (torch ops via ExternalStream)
+        d_step.zero_()
         dec.decode_device(d_y.data_ptr(), B, d_res.data_ptr(), d_l0.data_ptr(), d_st.data_ptr(),
                           dec.stream)
-        dec.count_device(d_tx.data_ptr(), d_res.data_ptr(), d_st.data_ptr(), B, d_cnt.data_ptr(),
+        dec.count_device(d_tx.data_ptr(), d_res.data_ptr(), d_st.data_ptr(), B, d_step.data_ptr(),
                          dec.stream)
-        if world > 1:
-            with torch.cuda.stream(stream):
-                dist.all_reduce(d_cnt)
+        reduce_step(d_step, d_cnt, world, dist)
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
@@ -155,28 +177,28 @@ def main():
         elapsed = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-    fast_ms, slow_ms, calls = dec.profile_read()
+    ms3, calls = dec.profile_read()
     dec.profile(False)
-    n_slow = dec.slow_count()
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    n_exact, n_coop = dec.path_counts()
+    elapsed = max_over_ranks(elapsed, world, dist, dev)
     cnt = d_cnt.cpu().numpy().astype(np.int64)  # summed over ranks (N > 1)
     total_words = world * B * args.steps
     value = total_words / elapsed
     # Algorithmic bytes per codeword: 8n B of f64 samples in, n B decoded bits and 8 B l0
-    # out. The fast kernel moves them for all B codewords; the exact kernel
-    # re-reads/writes them for the n_slow codewords handed to it.
+    # out. The fast kernel moves them for all B codewords; the exact and
+    # cooperative kernels re-read/write them for the codewords handed to them.
     bytes_per_cw = 9 * n + 8
     calls = max(1, calls)
-    k_fast = {"name": f"kaneko_fast_kernel<{args.m},{dec_tmax(args.t)}>", "ms": fast_ms / calls,
-              "codewords": B}
-    k_slow = {"name": f"kaneko_search_kernel<{args.m},{dec_tmax(args.t)}>", "ms": slow_ms / calls,
-              "codewords": int(n_slow) if fast_ms > 0 else B}
-    for k in (k_fast, k_slow):
+    tm = dec_tmax(args.t)
+    fast_on = ms3[0] > 0 and n_exact < B
+    kern = [{"name": f"kaneko_fast_kernel<{args.m},{tm}>", "ms": ms3[0] / calls, "codewords": B},
+            {"name": f"kaneko_search_kernel<{args.m},{tm}>", "ms": ms3[1] / calls,
+             "codewords": int(n_exact) if fast_on else B},
+            {"name": f"kaneko_coop_kernel<{args.m},{tm}>", "ms": ms3[2] / calls,
+             "codewords": int(n_coop)}]
+    for k in kern:
         k["GB_s"] = (bytes_per_cw * k["codewords"] / (k["ms"] / 1e3) / 1e9) if k["ms"] > 0 else 0.0
-    dom = k_fast if k_fast["ms"] >= k_slow["ms"] else k_slow
+    dom = max(kern, key=lambda k: k["ms"])
     achieved = dom["GB_s"]
     traffic = None
     if os.path.exists(args.traffic):
@@ -210,9 +232,10 @@ def main():
             "fer": (int(cnt[0]) / words) if words else None,
             "ber": (int(cnt[1]) / words / n) if words else None,
             "decodes_per_codeword": (int(cnt[2]) / words) if words else None,
-            "kernels": {"fast": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in k_fast.items()},
-                        "exact": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in k_slow.items()},
-                        "dominant": dom["name"]},
+            "kernels": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in kk.items()}
+                        for kk in kern],
+            "dominant_kernel": dom["name"],
+            "decode_ms": round(sum(k["ms"] for k in kern), 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic},

@@ -126,17 +126,19 @@ int bchk_sweep(bchk_ctx *ctx, long p, long e, double max_snr, uint64_t *rng_stat
 int bchk_sync(bchk_ctx *ctx);
 /* the context's HIP stream (hipStream_t) */
 void *bchk_stream(bchk_ctx *ctx);
-/* Kernel-time profiling with HIP events recorded on the launch stream around each
- * decode call: the lane-per-codeword fast kernel and the exact wave-per-codeword kernel
- * (which also runs alone when the fast path is off or unavailable). read() returns the
- * summed milliseconds since the last read and the number of decode calls, then resets. */
+/* Kernel-time profiling with HIP events recorded on the launch stream around each decode
+ * call's three stages: [0] the lane-per-codeword fast kernel (+ the control memset),
+ * [1] the exact wave-per-codeword kernel, [2] the workgroup-cooperative kernel for heavy
+ * codewords. read() returns the summed milliseconds per stage since the last read and the
+ * number of decode calls, then resets. */
 int bchk_profile(bchk_ctx *ctx, int enable);
-int bchk_profile_read(bchk_ctx *ctx, double *fast_ms, double *slow_ms, uint64_t *launches);
-/* Codewords the last decode call on the context's stream handed from the fast path to
- * the exact wave-per-codeword kernel (synchronises the context's stream). */
-int bchk_slow_count(bchk_ctx *ctx, uint64_t *count);
+int bchk_profile_read(bchk_ctx *ctx, double *ms3, uint64_t *launches);
+/* Codewords the last decode call handed from the fast path to the exact kernel, and from
+ * the exact kernel to the cooperative kernel (synchronises the context's stream). */
+int bchk_path_counts(bchk_ctx *ctx, uint64_t *to_exact, uint64_t *to_coop);
 /* Enable (default) or disable the fast path; results are identical either way. */
 int bchk_set_fast_path(bchk_ctx *ctx, int enable);
+
 const char *bchk_last_error(void);
 const char *bchk_version(void);
 

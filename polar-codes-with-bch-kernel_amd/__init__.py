@@ -31,7 +31,7 @@ EXPORTS = (
     "bchk_set_max_decodes", "bchk_decode_host", "bchk_decode_device",
     "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device",
     "bchk_generate_host", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
-    "bchk_profile_read", "bchk_slow_count", "bchk_set_fast_path", "bchk_last_error", "bchk_version",
+    "bchk_profile_read", "bchk_path_counts", "bchk_set_fast_path", "bchk_last_error", "bchk_version",
 )
 
 STATS_DTYPE = np.dtype([("decodes", "<u8"), ("comparisons", "<u8"), ("sums", "<u8"),
@@ -86,9 +86,9 @@ def lib():
     L.bchk_stream.argtypes = [vp]
     L.bchk_stream.restype = vp
     L.bchk_profile.argtypes = [vp, i32]
-    L.bchk_profile_read.argtypes = [vp, C.POINTER(dbl), C.POINTER(dbl), C.POINTER(u64)]
+    L.bchk_profile_read.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
     L.bchk_set_fast_path.argtypes = [vp, i32]
-    L.bchk_slow_count.argtypes = [vp, C.POINTER(u64)]
+    L.bchk_path_counts.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)]
     L.bchk_last_error.restype = C.c_char_p
     L.bchk_version.restype = C.c_char_p
     _lib = L
@@ -195,16 +195,17 @@ class KanekoKernelProcessor:
         _check(lib().bchk_profile(self._h, 1 if enable else 0))
 
     def profile_read(self):
-        """(fast-kernel ms, slow-kernel ms, decode calls) since the last read."""
-        a, b, n = C.c_double(), C.c_double(), C.c_uint64()
-        _check(lib().bchk_profile_read(self._h, C.byref(a), C.byref(b), C.byref(n)))
-        return a.value, b.value, n.value
-
-    def slow_count(self):
-        """Codewords the last decode handed to the exact wave-per-codeword kernel."""
+        """([fast, exact, coop] kernel ms summed, decode calls) since the last read."""
+        ms = (C.c_double * 3)()
         n = C.c_uint64()
-        _check(lib().bchk_slow_count(self._h, C.byref(n)))
-        return n.value
+        _check(lib().bchk_profile_read(self._h, ms, C.byref(n)))
+        return list(ms), n.value
+
+    def path_counts(self):
+        """(codewords handed to the exact kernel, to the cooperative kernel) last call."""
+        a, b = C.c_uint64(), C.c_uint64()
+        _check(lib().bchk_path_counts(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def set_fast_path(self, enable=True):
         _check(lib().bchk_set_fast_path(self._h, 1 if enable else 0))

@@ -44,6 +44,13 @@ struct SearchParams {
     uint32_t *heads;
     uint32_t *qtail;       // fast path: append unresolved codewords here (with queue_out)
     uint32_t *queue_out;
+    // heavy codewords: the wave kernel hands a codeword still running after chunk_limit
+    // steps of 64 patterns to the cooperative kernel (heavy_queue[*heavy_tail++]);
+    // heavy_tail == null disables the hand-off.
+    uint32_t *heavy_queue;
+    uint32_t *heavy_tail;
+    uint32_t *heavy_head;
+    uint32_t chunk_limit;
     int32_t t;
     int32_t J;             // < 0: shipped
     int32_t variant;       // BCHK_VARIANT_*

@@ -185,8 +185,10 @@ struct bchk_ctx {
     KernelSet ks{};
     FastFn fast = nullptr;
     bool use_fast = true;
-    size_t lds_fast = 0;
-    DevBuf queue, ctrl;  // slow-path work queue + {tail, 8 per-XCD heads} (128-B lines)
+    size_t lds_fast = 0, lds_coop = 0;
+    int grid_coop = 0;
+    uint32_t chunk_limit = 4;
+    DevBuf queue, heavy, ctrl;  // work queues + control words (one 128-B line each)
     uint8_t *d_tables = nullptr;
     hipStream_t stream = nullptr;
     size_t lds = 0, lds_alg = 0;
@@ -194,9 +196,9 @@ struct bchk_ctx {
     uint64_t max_decodes = 0;
     DevBuf y, res, l0, st, words, synd, ok;
     bool profile = false;
-    struct Ev { hipEvent_t a, b, c; };
+    struct Ev { hipEvent_t e[4]; };
     std::vector<Ev> events;
-    double prof_fast_ms = 0.0, prof_slow_ms = 0.0;
+    double prof_ms[3] = {0.0, 0.0, 0.0};
     uint64_t prof_launches = 0;
 };
 
@@ -209,12 +211,18 @@ int sigma_s2(int k, int n, double snr_db, double *sd) {
     return 0;
 }
 
-constexpr size_t kCtrlBytes = 9 * 128;  // tail at word 0, head x at word 32 (x + 1)
+// control block: fast-path queue tail (line 0), 8 per-XCD heads (lines 1-8), heavy-queue
+// tail (line 9) and head (line 10); zeroed by one memset per decode call
+constexpr size_t kCtrlBytes = 11 * 128;
+constexpr int kHeavyTail = 32 * 9, kHeavyHead = 32 * 10;
 
 int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t *d_res,
                   double *d_l0, bchk_stats *d_st, hipStream_t s) {
     if (B == 0) return 0;
     if (B > 0xFFFFFFFFull) return fail(BCHK_EINVAL, "batch too large");
+    int rc;
+    if ((rc = c->ctrl.ensure(kCtrlBytes)) || (rc = c->heavy.ensure(B * sizeof(uint32_t)))) return rc;
+    uint32_t *ctrl = (uint32_t *)c->ctrl.p;
     SearchParams p{};
     p.y = d_y;
     p.res = d_res;
@@ -228,39 +236,40 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     p.t = c->t;
     p.J = c->J;
     p.variant = variant;
-    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    p.heavy_queue = (uint32_t *)c->heavy.p;
+    p.heavy_tail = c->chunk_limit ? ctrl + kHeavyTail : nullptr;
+    p.heavy_head = ctrl + kHeavyHead;
+    p.chunk_limit = c->chunk_limit;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (c->profile) {
-        HIP_TRY(hipEventCreate(&e0));
-        HIP_TRY(hipEventCreate(&e1));
-        HIP_TRY(hipEventCreate(&e2));
-        HIP_TRY(hipEventRecord(e0, s));
+        for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventRecord(ev[0], s));
     }
+    HIP_TRY(hipMemsetAsync(ctrl, 0, kCtrlBytes, s));
     if (c->fast && c->use_fast) {
-        int rc;
-        if ((rc = c->queue.ensure(B * sizeof(uint32_t))) || (rc = c->ctrl.ensure(kCtrlBytes))) return rc;
-        uint32_t *ctrl = (uint32_t *)c->ctrl.p;
-        HIP_TRY(hipMemsetAsync(ctrl, 0, kCtrlBytes, s));
-        p.qtail = ctrl;
-        p.queue_out = (uint32_t *)c->queue.p;
-        HIP_TRY(c->fast(p, c->lds_fast, s));
-        if (c->profile) HIP_TRY(hipEventRecord(e1, s));
+        if ((rc = c->queue.ensure(B * sizeof(uint32_t)))) return rc;
+        SearchParams f = p;
+        f.qtail = ctrl;
+        f.queue_out = (uint32_t *)c->queue.p;
+        HIP_TRY(c->fast(f, c->lds_fast, s));
+        if (c->profile) HIP_TRY(hipEventRecord(ev[1], s));
         SearchParams q = p;
         q.queue = (const uint32_t *)c->queue.p;
         q.qcount = ctrl;
         q.heads = ctrl + 32;
-        q.qtail = nullptr;
-        q.queue_out = nullptr;
         // every resident wave may take work; waves beyond the queue length exit at once
         HIP_TRY(launch_search(c->ks, q, c->grid, c->lds, s));
     } else {
         const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
         const int grid = std::max(1, std::min(c->grid, need));
-        if (c->profile) HIP_TRY(hipEventRecord(e1, s));
+        if (c->profile) HIP_TRY(hipEventRecord(ev[1], s));
         HIP_TRY(launch_search(c->ks, p, grid, c->lds, s));
     }
+    if (c->profile) HIP_TRY(hipEventRecord(ev[2], s));
+    if (p.heavy_tail) HIP_TRY(c->ks.coop(p, c->grid_coop, c->lds_coop, s));
     if (c->profile) {
-        HIP_TRY(hipEventRecord(e2, s));
-        c->events.push_back({e0, e1, e2});
+        HIP_TRY(hipEventRecord(ev[3], s));
+        c->events.push_back({{ev[0], ev[1], ev[2], ev[3]}});
     }
     return 0;
 }
@@ -318,6 +327,18 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     c->lds_alg = tb;
     if (select_fast(m, t, &c->fast)) c->lds_fast = tb + kWavesPerBlock * fast_wave_bytes();
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
+    if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);
+    c->lds_coop = tb + c->ks.coop_bytes;
+    const void *cfn = c->ks.coop_ptr();
+    if (c->lds_coop > 65536)
+        (void)hipFuncSetAttribute(cfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_coop);
+    int coop_per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&coop_per_cu, cfn, kCoopThreads, c->lds_coop) != hipSuccess ||
+        coop_per_cu <= 0) {
+        coop_per_cu = 1;
+        (void)hipGetLastError();
+    }
+    c->grid_coop = coop_per_cu * prop.multiProcessorCount;
     const void *fn = c->ks.search_ptr();
     if (c->lds > 65536)
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
@@ -335,12 +356,10 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
 
 void bchk_destroy(bchk_ctx *c) {
     if (!c) return;
-    for (auto &e : c->events) {
-        (void)hipEventDestroy(e.a);
-        (void)hipEventDestroy(e.b);
-        (void)hipEventDestroy(e.c);
-    }
+    for (auto &e : c->events)
+        for (auto &x : e.e) (void)hipEventDestroy(x);
     c->queue.release();
+    c->heavy.release();
     c->ctrl.release();
     c->y.release();
     c->res.release();
@@ -580,37 +599,38 @@ int bchk_profile(bchk_ctx *c, int enable) {
     return 0;
 }
 
-int bchk_profile_read(bchk_ctx *c, double *fast_ms, double *slow_ms, uint64_t *launches) {
+int bchk_profile_read(bchk_ctx *c, double *ms3, uint64_t *launches) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
     for (auto &e : c->events) {
-        HIP_TRY(hipEventSynchronize(e.c));
-        float a = 0.f, b = 0.f;
-        HIP_TRY(hipEventElapsedTime(&a, e.a, e.b));
-        HIP_TRY(hipEventElapsedTime(&b, e.b, e.c));
-        c->prof_fast_ms += a;
-        c->prof_slow_ms += b;
+        HIP_TRY(hipEventSynchronize(e.e[3]));
+        for (int k = 0; k < 3; ++k) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, e.e[k], e.e[k + 1]));
+            c->prof_ms[k] += ms;
+        }
         c->prof_launches += 1;
-        (void)hipEventDestroy(e.a);
-        (void)hipEventDestroy(e.b);
-        (void)hipEventDestroy(e.c);
+        for (auto &x : e.e) (void)hipEventDestroy(x);
     }
     c->events.clear();
-    if (fast_ms) *fast_ms = c->prof_fast_ms;
-    if (slow_ms) *slow_ms = c->prof_slow_ms;
+    if (ms3)
+        for (int k = 0; k < 3; ++k) ms3[k] = c->prof_ms[k];
     if (launches) *launches = c->prof_launches;
-    c->prof_fast_ms = c->prof_slow_ms = 0.0;
+    c->prof_ms[0] = c->prof_ms[1] = c->prof_ms[2] = 0.0;
     c->prof_launches = 0;
     return 0;
 }
 
-int bchk_slow_count(bchk_ctx *c, uint64_t *count) {
-    if (!c || !count) return fail(BCHK_EINVAL, "NULL argument");
-    *count = 0;
-    if (!c->ctrl.p) return 0;
-    uint32_t v = 0;
-    HIP_TRY(hipMemcpyAsync(&v, c->ctrl.p, sizeof v, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    *count = v;
+int bchk_path_counts(bchk_ctx *c, uint64_t *to_exact, uint64_t *to_coop) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    uint32_t v[2] = {0, 0};
+    if (c->ctrl.p) {
+        HIP_TRY(hipMemcpyAsync(&v[0], (uint32_t *)c->ctrl.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&v[1], (uint32_t *)c->ctrl.p + kHeavyTail, 4, hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    if (to_exact) *to_exact = v[0];
+    if (to_coop) *to_coop = v[1];
     return 0;
 }
 

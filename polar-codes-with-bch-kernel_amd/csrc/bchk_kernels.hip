@@ -32,34 +32,44 @@ namespace bchk {
 template <int M, int TMAX>
 struct Smem {
     static constexpr int NP = 64 * Geo<M>::NW;     // padded positions per wave
-    static constexpr int WAVE_BYTES = NP * 8 + NP; // sorted |alpha| (f64) + order (u8)
+    // sorted |alpha| (f64), |alpha| by position (f64), order (u8)
+    static constexpr int WAVE_BYTES = NP * 8 * 2 + NP;
+};
+constexpr int kCoopWaves = 16;  // waves that share one heavy codeword (1024 threads)
+
+// ------------------------------------------------------- per-codeword prep
+// Reference: KanekoKernelProcessor::decode(answer, word, res) prologue and set-up,
+// src/KanekoKernelProcessor.cpp:336-359 (and :213-234 for decode(word, res)).
+template <int M, int TMAX>
+struct Prep {
+    static constexpr int NW = Geo<M>::NW, W = (TMAX + 3) / 4;
+    double av[NW];     // |alpha| of position lane + 64 s
+    double asv[NW];    // sorted |alpha|, rank lane + 64 s
+    int ordv[NW];      // position of rank lane + 64 s
+    Mask<NW> yH;       // hard decision (wave-uniform)
+    uint32_t S0[W];    // odd syndromes of yH (wave-uniform)
+    uint32_t scol[W];  // lane b: odd-syndrome column of position ord[b]
+    int ordb;          // lane b: ord[b]
+    uint32_t Lo[W];    // syndrome contribution of pattern bits 0..5 = lane
+    Mask<NW> Plo;      // flipped positions of pattern bits 0..5 = lane
+    bool tie;          // two |alpha| exactly equal
 };
 
-// ---------------------------------------------------------- Kaneko search
-// One codeword per wave. Reference: KanekoKernelProcessor::decode(answer, word, res)
-// src/KanekoKernelProcessor.cpp:335-407 (variant ANSWER) and decode(word, res) :212-276
-// (variant WORD).
 template <int M, int TMAX>
-__device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const uint16_t *lg,
-                                const uint32_t *col, const uint64_t *chien, double *as,
-                                uint8_t *ordl, uint32_t cw, int lane) {
-    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
-    constexpr int W = (TMAX + 3) / 4;
+__device__ void prep_codeword(const SearchParams &p, const uint32_t *col, double *as, double *ap,
+                              uint8_t *ordl, uint32_t cw, int lane, Prep<M, TMAX> &P) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
     constexpr int NB = N < 31 ? N : 31;  // pattern bits in use (i < 2^31)
-    const int t = p.t;
     const double *y = p.y + (size_t)cw * N;
-
-    // ---- prologue :336-343: alpha = 2*word/pow(sd,2); yH; |alpha|
-    double av[NW];
-    Mask<NW> yH;
+    // alpha = 2*word/pow(sd,2); yH; |alpha| (:336-342)
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         const int pos = lane + 64 * s;
         const bool valid = pos < N;
         const double yy = valid ? y[pos] : 0.0;
         const double al = (2.0 * yy) / p.s2;
-        av[s] = valid ? fabs(al) : 0.0;
-        yH.w[s] = ballot(valid && !(al <= 0.0));
+        P.av[s] = valid ? fabs(al) : 0.0;
+        P.yH.w[s] = ballot(valid && !(al <= 0.0));
     }
     // exact rank by (|alpha|, position): the stable order of std::sort's keys (:343)
     int rk[NW];
@@ -68,220 +78,286 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     for (int s = 0; s < NW; ++s) rk[s] = 0;
 #pragma unroll
     for (int q = 0; q < N; ++q) {
-        const double aq = rdlf(av[q >> 6], q & 63);
+        const double aq = rdlf(P.av[q >> 6], q & 63);
 #pragma unroll
         for (int s = 0; s < NW; ++s) {
             const int pos = lane + 64 * s;
-            const bool lt = aq < av[s];
-            const bool eq = aq == av[s];
+            const bool lt = aq < P.av[s];
+            const bool eq = aq == P.av[s];
             rk[s] += (lt || (eq && q < pos)) ? 1 : 0;
             tie |= eq && (q != pos) && (pos < N);
         }
     }
-    const bool any_tie = ballot(tie) != 0;
+    P.tie = ballot(tie) != 0;
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         const int pos = lane + 64 * s;
         if (pos < N) {
-            as[rk[s]] = av[s];
+            as[rk[s]] = P.av[s];
+            ap[pos] = P.av[s];
             ordl[rk[s]] = (uint8_t)pos;
         }
     }
     wave_sync();
-    double asv[NW];  // sorted |alpha|, lane owns q = lane + 64 s
-    int ordv[NW];
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         const int q = lane + 64 * s;
-        asv[s] = q < N ? as[q] : 0.0;
-        ordv[s] = q < N ? ordl[q] : 0;
+        P.asv[s] = q < N ? as[q] : 0.0;
+        P.ordv[s] = q < N ? ordl[q] : 0;
     }
-
-    // ---- syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
-    uint32_t S0[W];
+    // syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
 #pragma unroll
-    for (int w = 0; w < W; ++w) S0[w] = 0;
+    for (int w = 0; w < W; ++w) P.S0[w] = 0;
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         const int pos = lane + 64 * s;
-        if (pos < N && ((yH.w[s] >> lane) & 1ull)) {
+        if (pos < N && ((P.yH.w[s] >> lane) & 1ull)) {
 #pragma unroll
-            for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w];
+            for (int w = 0; w < W; ++w) P.S0[w] ^= col[pos * W + w];
         }
     }
 #pragma unroll
-    for (int w = 0; w < W; ++w) S0[w] = wave_xor(S0[w]);
-
-    // ---- test patterns (calcError :36-51): bit b of i flips position ord[b].
-    // lane b < NB holds ord[b] and its syndrome column.
-    const int ordb = ordv[0];
-    uint32_t scol[W];
+    for (int w = 0; w < W; ++w) P.S0[w] = wave_xor(P.S0[w]);
+    // test patterns (calcError :36-51): bit b of i flips position ord[b]
+    P.ordb = P.ordv[0];
 #pragma unroll
-    for (int w = 0; w < W; ++w) scol[w] = lane < NB ? col[ordb * W + w] : 0u;
-    uint32_t Lo[W];
-    Mask<NW> Plo;
+    for (int w = 0; w < W; ++w) P.scol[w] = lane < NB ? col[P.ordb * W + w] : 0u;
 #pragma unroll
-    for (int w = 0; w < W; ++w) Lo[w] = 0;
+    for (int w = 0; w < W; ++w) P.Lo[w] = 0;
 #pragma unroll
-    for (int s = 0; s < NW; ++s) Plo.w[s] = 0;
+    for (int s = 0; s < NW; ++s) P.Plo.w[s] = 0;
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
         if (b < NB) {
             const bool on = (lane >> b) & 1;
-            const int pb = (int)rdl((uint32_t)ordb, b);
+            const int pb = (int)rdl((uint32_t)P.ordb, b);
 #pragma unroll
-            for (int w = 0; w < W; ++w) Lo[w] ^= on ? rdl(scol[w], b) : 0u;
-            if (on) mask_set<NW>(Plo, pb);
+            for (int w = 0; w < W; ++w) P.Lo[w] ^= on ? rdl(P.scol[w], b) : 0u;
+            if (on) mask_set<NW>(P.Plo, pb);
         }
     }
+}
 
-    // ---- search state (:351-358)
-    const bool word_variant = p.variant == BCHK_VARIANT_WORD;
-    const uint64_t kInfBound = 0x7FFFFFFFFFFFFFFFull;
-    int T = N;
-    uint64_t bound = word_variant ? kInfBound : ((1ull << (T & 31)) - 1ull);
-    double l0 = DBL_MAX;
-    bool firstOK = true, accepted = false, returned = false, truncated = false, scan_ub = false;
-    int m0 = 0;
+// Decode test patterns i = base + lane (base a multiple of 64): returns success and
+// diff = yH ^ x (flipped pattern positions ^ error locations); for successful lanes also
+// m = calcM (:89-97) and l = calcL (:69-77), summed over diff in index order from the
+// wave's |alpha|-by-position LDS slice (lane-parallel; the ordered acceptance only
+// compares them).
+template <int M, int TMAX>
+__device__ __forceinline__ bool decode_chunk(const Prep<M, TMAX> &P, uint64_t base, int t,
+                                             const uint8_t *ex, const uint16_t *lg,
+                                             const uint64_t *chien, const double *ap,
+                                             Mask<Geo<M>::NW> &diff, int &m, double &l) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
+    constexpr int NB = N < 31 ? N : 31;
+    uint32_t Sw[W];
+    Mask<NW> Pm = P.Plo;
+#pragma unroll
+    for (int w = 0; w < W; ++w) Sw[w] = P.S0[w] ^ P.Lo[w];
+    for (uint64_t hb = base >> 6; hb; hb &= hb - 1) {  // high pattern bits: wave-uniform
+        const int b = 6 + (int)__builtin_ctzll(hb);
+        if (b >= NB) continue;
+        const int pb = (int)rdl((uint32_t)P.ordb, b);
+#pragma unroll
+        for (int w = 0; w < W; ++w) Sw[w] ^= rdl(P.scol[w], b);
+        mask_set<NW>(Pm, pb);
+    }
+    Mask<NW> E;
+    const bool ok = alg_core<M, TMAX>(ex, lg, chien, Sw, t, E);
+#pragma unroll
+    for (int s = 0; s < NW; ++s) diff.w[s] = Pm.w[s] ^ E.w[s];
+    m = 0;
+    l = 0.0;
+    if (ok) {
+        m = mask_popc<NW>(diff);
+#pragma unroll
+        for (int s = 0; s < NW; ++s)
+            for (uint64_t v = diff.w[s]; v; v &= v - 1) l += ap[64 * s + (int)__builtin_ctzll(v)];
+    }
+    return ok;
+}
+
+// ----------------------------------------------------- sequential search state
+template <int NW>
+struct SearchState {
+    double l0;
+    uint64_t bound, jsteps, impr, i_end;
     Mask<NW> best;
-#pragma unroll
-    for (int s = 0; s < NW; ++s) best.w[s] = 0;
-    uint64_t jsteps = 0, impr = 0, i_end = 0;
-    const int scan_last = N - 1 - t;  // j <= n-1-t (:384)
+    int T, m0;
+    bool firstOK, accepted, returned, truncated, scan_ub, done;
+};
 
-    for (uint64_t base = 0;; base += 64) {
-        if (base >= bound) { i_end = bound; break; }
-        if (p.max_decodes && base >= p.max_decodes) { i_end = base; truncated = true; break; }
-        // high pattern bits of base (bits >= 6): wave-uniform
-        uint32_t Sw[W];
-        Mask<NW> P = Plo;
+template <int M>
+__device__ __forceinline__ void init_state(SearchState<Geo<M>::NW> &S, int variant) {
+    constexpr int N = Geo<M>::N;
+    S.T = N;  // :354 (ANSWER); LONG_MAX sentinel for WORD (:229)
+    S.bound = variant == BCHK_VARIANT_WORD ? 0x7FFFFFFFFFFFFFFFull : ((1ull << (S.T & 31)) - 1ull);
+    S.l0 = DBL_MAX;
+    S.m0 = 0;
+    S.jsteps = S.impr = S.i_end = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) Sw[w] = S0[w] ^ Lo[w];
-        for (uint64_t hb = base >> 6; hb; hb &= hb - 1) {
-            const int b = 6 + (int)__builtin_ctzll(hb);
-            if (b >= NB) continue;
-            const int pb = (int)rdl((uint32_t)ordb, b);
-#pragma unroll
-            for (int w = 0; w < W; ++w) Sw[w] ^= rdl(scol[w], b);
-            mask_set<NW>(P, pb);
-        }
-        Mask<NW> E;
-        const bool ok = alg_core<M, TMAX>(ex, lg, chien, Sw, t, E);
-        Mask<NW> diff;  // yH ^ x = pattern ^ error locations
-#pragma unroll
-        for (int s = 0; s < NW; ++s) diff.w[s] = P.w[s] ^ E.w[s];
-        const uint64_t i_lane = base + (uint64_t)lane;
-        uint64_t okm = ballot(ok && i_lane < bound);
-        if (base == 0 && !(okm & 1ull)) firstOK = false;  // :371
+    for (int s = 0; s < Geo<M>::NW; ++s) S.best.w[s] = 0;
+    S.firstOK = true;
+    S.accepted = S.returned = S.truncated = S.scan_ub = S.done = false;
+}
 
-        bool done = false;
-        while (okm) {
-            const int L = (int)__builtin_ctzll(okm);
-            okm &= okm - 1;
-            const uint64_t ii = base + (uint64_t)L;
-            if (ii >= bound) break;
-            Mask<NW> d;
+// One successful decode at test pattern ii, in pattern order: the body of the reference
+// loop after `success` (:372-398). Wave-uniform inputs; the calcT scan is lane-parallel.
+// Sets S.done when the reference loop would end after this iteration.
+template <int M, int TMAX>
+__device__ void accept_success(SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
+                               const Mask<Geo<M>::NW> &d, int m, double l, uint64_t ii,
+                               const double *as, const SearchParams &p, int lane) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    const int t = p.t;
+    if (ii == 0 || !S.firstOK) S.m0 = m; // :374 (m = calcM, l = calcL of this candidate)
+    if (!(l < S.l0)) return;             // :377
+    S.best = d;                          // res = x; l0 = l (:378-379)
+    S.l0 = l;
+    S.accepted = true;
+    // calcRightSide :54-67 and the calcT prefix (:110-121) over agreeing sorted positions;
+    // both are prefixes of the same sequential sum.
+    const int border = (2 * t + 1) - (m + S.m0) / 2;
+    const int border2 = t - (m + S.m0) / 2;
+    double rs = 0.0, base2 = 0.0;
+    int taken = 0;
 #pragma unroll
-            for (int s = 0; s < NW; ++s) d.w[s] = rdl64(diff.w[s], L);
-            const int m = mask_popc<NW>(d);                 // calcM :89-97
-            if (ii == 0 || !firstOK) m0 = m;                 // :374
-            double l = 0.0;                                  // calcL :69-77, index order
+    for (int s = 0; s < NW; ++s) {
+        const int q = lane + 64 * s;
+        const int op = P.ordv[s];
+        uint64_t dw = 0;
 #pragma unroll
-            for (int s = 0; s < NW; ++s)
-                for (uint64_t v = d.w[s]; v; v &= v - 1) l += rdlf(av[s], (int)__builtin_ctzll(v));
-            if (!(l < l0)) continue;                         // :377
-            // res = x; l0 = l (:378-379)
-            best = d;
-            l0 = l;
-            accepted = true;
-            // calcRightSide :54-67 and the calcT prefix (:110-121) over agreeing sorted
-            // positions; both are prefixes of the same sequential sum.
-            const int border = (2 * t + 1) - (m + m0) / 2;
-            const int border2 = t - (m + m0) / 2;
-            double rs = 0.0, base2 = 0.0;
-            int taken = 0;
-            if (border2 <= 0) base2 = 0.0;
-#pragma unroll
-            for (int s = 0; s < NW; ++s) {
-                const int q = lane + 64 * s;
-                const int op = ordv[s];
-                uint64_t dw = 0;
-#pragma unroll
-                for (int u = 0; u < NW; ++u) dw = (u == (op >> 6)) ? d.w[u] : dw;
-                const bool ag = q < N && !((dw >> (op & 63)) & 1ull);
-                uint64_t agm = ballot(ag);
-                while (agm && taken < border) {
-                    const int b = (int)__builtin_ctzll(agm);
-                    agm &= agm - 1;
-                    rs += rdlf(asv[s], b);
-                    ++taken;
-                    if (taken == border2) base2 = rs;
-                }
-            }
-            if (l < rs) { returned = true; i_end = ii + 1; done = true; break; }  // :380
-            // calcT scan (:384): while (l >= calcT(j) && j <= n-1-t) ++j, lane-parallel
-            int jstar;
-            {
-                int first = 0x7FFFFFFF;
-#pragma unroll
-                for (int s = 0; s < (N + 63) / 64; ++s) {
-                    const int j = lane + 64 * s;
-                    bool stop = true;  // j beyond the scan range stops it
-                    if (j <= scan_last) {
-                        double ct = base2;
-                        for (int u = 0; u <= t; ++u) ct += as[j + u];
-                        stop = !(l >= ct);
-                    }
-                    const uint64_t sm = ballot(stop && j < N);
-                    if (sm && first == 0x7FFFFFFF) first = 64 * s + (int)__builtin_ctzll(sm);
-                }
-                jstar = first;
-                if (jstar > scan_last + 1) jstar = scan_last + 1;
-            }
-            if (word_variant && jstar == scan_last + 1) scan_ub = true;  // :257 unbounded
-            jsteps += (uint64_t)jstar;
-            ++impr;
-            if (word_variant) {
-                T = jstar;                                   // :264
-                bound = 1ull << (T & 63);
-            } else {
-                T = (p.J >= 0 && jstar > p.J) ? p.J : jstar;  // :392 / :393
-                bound = (1ull << (T & 31)) - 1ull;           // (1 << T) - 1 in int32 (:361)
-            }
-            if (bound <= ii + 1) { i_end = ii + 1; done = true; break; }
+        for (int u = 0; u < NW; ++u) dw = (u == (op >> 6)) ? d.w[u] : dw;
+        const bool ag = q < N && !((dw >> (op & 63)) & 1ull);
+        uint64_t agm = ballot(ag);
+        while (agm && taken < border) {
+            const int b = (int)__builtin_ctzll(agm);
+            agm &= agm - 1;
+            rs += rdlf(P.asv[s], b);
+            ++taken;
+            if (taken == border2) base2 = rs;
         }
-        if (done) break;
     }
+    if (l < rs) {                        // :380-382
+        S.returned = true;
+        S.i_end = ii + 1;
+        S.done = true;
+        return;
+    }
+    // calcT scan (:384): while (l >= calcT(j) && j <= n-1-t) ++j, one j per lane
+    const int scan_last = N - 1 - t;
+    int first = 0x7FFFFFFF;
+#pragma unroll
+    for (int s = 0; s < (N + 63) / 64; ++s) {
+        const int j = lane + 64 * s;
+        bool stop = true;  // j beyond the scan range stops it
+        if (j <= scan_last) {
+            double ct = base2;
+            for (int u = 0; u <= t; ++u) ct += as[j + u];
+            stop = !(l >= ct);
+        }
+        const uint64_t sm = ballot(stop && j < N);
+        if (sm && first == 0x7FFFFFFF) first = 64 * s + (int)__builtin_ctzll(sm);
+    }
+    const int jstar = first > scan_last + 1 ? scan_last + 1 : first;
+    const bool word_variant = p.variant == BCHK_VARIANT_WORD;
+    if (word_variant && jstar == scan_last + 1) S.scan_ub = true;  // :257 unbounded
+    S.jsteps += (uint64_t)jstar;
+    ++S.impr;
+    if (word_variant) {
+        S.T = jstar;                                     // :264
+        S.bound = 1ull << (S.T & 63);
+    } else {
+        S.T = (p.J >= 0 && jstar > p.J) ? p.J : jstar;   // :392 / :393
+        S.bound = (1ull << (S.T & 31)) - 1ull;           // (1 << T) - 1 in int32 (:361)
+    }
+    if (S.bound <= ii + 1) {
+        S.i_end = ii + 1;
+        S.done = true;
+    }
+}
 
-    // ---- outputs
-    const uint64_t decodes = i_end;
-    const uint64_t iters = returned ? i_end - 1 : i_end;
+template <int M, int TMAX>
+__device__ void write_outputs(const SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
+                              const SearchParams &p, uint32_t cw, int lane) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    const bool word_variant = p.variant == BCHK_VARIANT_WORD;
+    const uint64_t decodes = S.i_end;
+    const uint64_t iters = S.returned ? S.i_end - 1 : S.i_end;
     const uint64_t pro = word_variant ? (uint64_t)(2 * N + 1) : 0ull;  // :221-224
-    if (accepted) {
+    if (S.accepted) {
 #pragma unroll
         for (int s = 0; s < NW; ++s) {
             const int pos = lane + 64 * s;
             if (pos < N)
-                p.res[(size_t)cw * N + pos] = (uint8_t)(((yH.w[s] ^ best.w[s]) >> lane) & 1ull);
+                p.res[(size_t)cw * N + pos] = (uint8_t)(((P.yH.w[s] ^ S.best.w[s]) >> lane) & 1ull);
         }
     }
     if (lane == 0) {
-        if (p.l0) p.l0[cw] = l0;
+        if (p.l0) p.l0[cw] = S.l0;
         if (p.st) {
             bchk_stats st;
             st.decodes = decodes;
-            st.comparisons = pro + iters * (uint64_t)(N + 6) + jsteps + impr;
-            st.sums = pro + iters * (uint64_t)(N + 1) + jsteps;
+            st.comparisons = pro + iters * (uint64_t)(N + 6) + S.jsteps + S.impr;
+            st.sums = pro + iters * (uint64_t)(N + 1) + S.jsteps;
             st.iterations = iters;
-            st.jsteps = jsteps;
-            st.improvements = impr;
-            st.flags = (accepted ? BCHK_F_ACCEPTED : 0u) | (returned ? BCHK_F_RETURNED : 0u) |
-                       (truncated ? BCHK_F_TRUNCATED : 0u) | (any_tie ? BCHK_F_TIE : 0u) |
-                       (scan_ub ? BCHK_F_SCAN_UB : 0u);
+            st.jsteps = S.jsteps;
+            st.improvements = S.impr;
+            st.flags = (S.accepted ? BCHK_F_ACCEPTED : 0u) | (S.returned ? BCHK_F_RETURNED : 0u) |
+                       (S.truncated ? BCHK_F_TRUNCATED : 0u) | (P.tie ? BCHK_F_TIE : 0u) |
+                       (S.scan_ub ? BCHK_F_SCAN_UB : 0u);
             st.reserved = 0;
             p.st[cw] = st;
         }
     }
+}
+
+// ------------------------------------------------ wave-per-codeword search
+// 64 consecutive test patterns per step, acceptance in pattern order. A codeword still
+// running after p.chunk_limit steps is handed to the cooperative kernel (heavy queue).
+template <int M, int TMAX>
+__device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const uint16_t *lg,
+                                const uint32_t *col, const uint64_t *chien, double *as,
+                                double *ap, uint8_t *ordl, uint32_t cw, int lane) {
+    constexpr int NW = Geo<M>::NW;
+    Prep<M, TMAX> P;
+    prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+    SearchState<NW> S;
+    init_state<M>(S, p.variant);
+    uint32_t chunks = 0;
+    for (uint64_t base = 0;; base += 64, ++chunks) {
+        if (base >= S.bound) { S.i_end = S.bound; break; }
+        if (p.max_decodes && base >= p.max_decodes) { S.i_end = base; S.truncated = true; break; }
+        if (p.heavy_tail && chunks == p.chunk_limit) {
+            if (lane == 0) p.heavy_queue[atomicAdd(p.heavy_tail, 1u)] = cw;
+            return;  // redone from scratch by kaneko_coop_kernel
+        }
+        Mask<NW> diff;
+        int m;
+        double l;
+        const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, diff, m, l);
+        uint64_t okm = ballot(ok && base + (uint64_t)lane < S.bound);
+        if (base == 0 && !(okm & 1ull)) S.firstOK = false;  // :371
+        while (okm) {
+            const int L = (int)__builtin_ctzll(okm);
+            okm &= okm - 1;
+            const uint64_t ii = base + (uint64_t)L;
+            if (ii >= S.bound) break;
+            const double lL = rdlf(l, L);
+            const int mL = (int)rdl((uint32_t)m, L);
+            if (!(lL < S.l0)) {  // not an improvement: only the m0 update (:374)
+                if (ii == 0 || !S.firstOK) S.m0 = mL;
+                continue;
+            }
+            Mask<NW> d;
+#pragma unroll
+            for (int s = 0; s < NW; ++s) d.w[s] = rdl64(diff.w[s], L);
+            accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
+            if (S.done) break;
+        }
+        if (S.done) break;
+    }
+    write_outputs<M, TMAX>(S, P, p, cw, lane);
 }
 
 template <int M, int TMAX>
@@ -298,16 +374,18 @@ kaneko_search_kernel(SearchParams p) {
     constexpr int NP = Smem<M, TMAX>::NP;
     uint8_t *wbase = smem + ((p.td.bytes + 15) & ~15u) + wid * Smem<M, TMAX>::WAVE_BYTES;
     double *as = reinterpret_cast<double *>(wbase);
-    uint8_t *ordl = wbase + NP * 8;
+    double *ap = as + NP;
+    uint8_t *ordl = wbase + NP * 16;
     if (!p.queue) {
         const uint32_t stride = gridDim.x * kWavesPerBlock;
         for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride)
-            search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ordl, cw, lane);
+            search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ap, ordl, cw, lane);
         return;
     }
     // Work queue left by the fast path: sub-queue x holds items x, x+8, x+16, ...; a wave
     // drains its own XCD's sub-queue first (one L2-local atomic per codeword), then steals.
     const uint32_t total = *p.qcount;
+    if ((blockIdx.x * kWavesPerBlock + wid) >= total) return;  // more waves than work
     int x = xcc_id();
     for (int exhausted = 0; exhausted < 8;) {
         uint32_t k = 0;
@@ -319,7 +397,106 @@ kaneko_search_kernel(SearchParams p) {
             ++exhausted;
             continue;
         }
-        search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ordl, p.queue[item], lane);
+        search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane);
+    }
+}
+
+// ---------------------------------------- cooperative search of heavy codewords
+// One workgroup of kCoopWaves waves per codeword: every round, wave w decodes patterns
+// [base + 64 w, base + 64 w + 64); wave 0 then applies the reference's sequential
+// acceptance to all successes of the round in pattern order (:361-405) and publishes the
+// new loop bound. Results are identical to the single-wave search.
+template <int M, int TMAX>
+__global__ void __launch_bounds__(kWaveSize * kCoopWaves)
+kaneko_coop_kernel(SearchParams p) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    constexpr int NP = Smem<M, TMAX>::NP;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    load_tables(smem, p.tables, p.td.bytes);
+    const uint8_t *ex = smem + p.td.off_exp;
+    const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
+    const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
+    const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint8_t *shared0 = smem + ((p.td.bytes + 15) & ~15u);
+    uint64_t *okm_l = reinterpret_cast<uint64_t *>(shared0);                    // [waves]
+    uint64_t *diff_l = okm_l + kCoopWaves;                                      // [waves][64][NW]
+    double *l_l = reinterpret_cast<double *>(diff_l + kCoopWaves * 64 * NW);    // [waves][64]
+    uint32_t *m_l = reinterpret_cast<uint32_t *>(l_l + kCoopWaves * 64);        // [waves][64]
+    uint64_t *ctl = reinterpret_cast<uint64_t *>(m_l + kCoopWaves * 64);        // bound, done, item
+    uint8_t *wbase = reinterpret_cast<uint8_t *>(ctl + 4) + wid * Smem<M, TMAX>::WAVE_BYTES;
+    double *as = reinterpret_cast<double *>(wbase);
+    double *ap = as + NP;
+    uint8_t *ordl = wbase + NP * 16;
+    const uint32_t total = *p.heavy_tail;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) ctl[2] = atomicAdd(p.heavy_head, 1u);
+        __syncthreads();
+        const uint32_t item = (uint32_t)ctl[2];
+        if (item >= total) return;
+        const uint32_t cw = p.heavy_queue[item];
+        Prep<M, TMAX> P;  // every wave builds the same prep (its own LDS slice)
+        prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+        SearchState<NW> S;
+        init_state<M>(S, p.variant);
+        if (threadIdx.x == 0) { ctl[0] = S.bound; ctl[1] = 0; }
+        for (uint64_t rbase = 0;; rbase += 64 * kCoopWaves) {
+            __syncthreads();
+            const uint64_t bound = ctl[0];
+            if (ctl[1]) break;
+            const uint64_t base = rbase + 64 * (uint64_t)wid;
+            uint64_t okm = 0;
+            if (base < bound && !(p.max_decodes && base >= p.max_decodes)) {
+                Mask<NW> diff;
+                int m;
+                double l;
+                const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, diff, m, l);
+                okm = ballot(ok && base + (uint64_t)lane < bound);
+                if (ok) {
+#pragma unroll
+                    for (int s = 0; s < NW; ++s) diff_l[(wid * 64 + lane) * NW + s] = diff.w[s];
+                    l_l[wid * 64 + lane] = l;
+                    m_l[wid * 64 + lane] = (uint32_t)m;
+                }
+            }
+            if (lane == 0) okm_l[wid] = okm;
+            __syncthreads();
+            if (wid == 0) {
+                for (int w = 0; w < kCoopWaves && !S.done; ++w) {
+                    const uint64_t bw = rbase + 64 * (uint64_t)w;
+                    if (bw >= S.bound) { S.i_end = S.bound; S.done = true; break; }
+                    if (p.max_decodes && bw >= p.max_decodes) {
+                        S.i_end = bw;
+                        S.truncated = true;
+                        S.done = true;
+                        break;
+                    }
+                    uint64_t m = okm_l[w];
+                    if (bw == 0 && !(m & 1ull)) S.firstOK = false;  // :371
+                    while (m) {
+                        const int L = (int)__builtin_ctzll(m);
+                        m &= m - 1;
+                        const uint64_t ii = bw + (uint64_t)L;
+                        if (ii >= S.bound) break;
+                        const double lL = l_l[w * 64 + L];
+                        const int mL = (int)m_l[w * 64 + L];
+                        if (!(lL < S.l0)) {  // not an improvement: only the m0 update (:374)
+                            if (ii == 0 || !S.firstOK) S.m0 = mL;
+                            continue;
+                        }
+                        Mask<NW> d;
+#pragma unroll
+                        for (int s = 0; s < NW; ++s) d.w[s] = diff_l[(w * 64 + L) * NW + s];
+                        accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
+                        if (S.done) break;
+                    }
+                }
+                if (lane == 0) { ctl[0] = S.bound; ctl[1] = S.done ? 1u : 0u; }
+            }
+        }
+        if (wid == 0) write_outputs<M, TMAX>(S, P, p, cw, lane);
+        (void)N;
     }
 }
 
@@ -400,6 +577,12 @@ static hipError_t launch_search_impl(const SearchParams &p, int grid, size_t lds
     return hipGetLastError();
 }
 template <int M, int TMAX>
+static hipError_t launch_coop_impl(const SearchParams &p, int grid, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((kaneko_coop_kernel<M, TMAX>), dim3(grid), dim3(kWaveSize * kCoopWaves),
+                       lds, s, p);
+    return hipGetLastError();
+}
+template <int M, int TMAX>
 static hipError_t launch_alg_impl(const AlgParams &p, size_t lds, hipStream_t s) {
     const int grid = (int)((p.count + 255) / 256);
     hipLaunchKernelGGL((alg_decode_kernel<M, TMAX>), dim3(grid), dim3(256), lds, s, p);
@@ -407,12 +590,18 @@ static hipError_t launch_alg_impl(const AlgParams &p, size_t lds, hipStream_t s)
 }
 template <int M, int TMAX>
 static const void *search_fn() { return reinterpret_cast<const void *>(&kaneko_search_kernel<M, TMAX>); }
-
+template <int M, int TMAX>
+static const void *coop_fn() { return reinterpret_cast<const void *>(&kaneko_coop_kernel<M, TMAX>); }
 
 template <int M, int TMAX>
 static KernelSet make_set() {
-    return KernelSet{&launch_search_impl<M, TMAX>, &launch_alg_impl<M, TMAX>, &search_fn<M, TMAX>,
-                     TMAX, (size_t)Smem<M, TMAX>::WAVE_BYTES};
+    constexpr int NW = Geo<M>::NW;
+    const size_t coop = (size_t)kCoopWaves * 8 + (size_t)kCoopWaves * 64 * NW * 8 +
+                        (size_t)kCoopWaves * 64 * 12 + 32 +
+                        (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES;
+    return KernelSet{&launch_search_impl<M, TMAX>, &launch_coop_impl<M, TMAX>, &coop_fn<M, TMAX>, coop,
+                     &launch_alg_impl<M, TMAX>, &search_fn<M, TMAX>, TMAX,
+                     (size_t)Smem<M, TMAX>::WAVE_BYTES};
 }
 
 // TMAX buckets: smallest instantiated bucket >= t.

@@ -8,6 +8,9 @@ namespace bchk {
 
 struct KernelSet {
     hipError_t (*search)(const SearchParams &, int, size_t, hipStream_t);
+    hipError_t (*coop)(const SearchParams &, int, size_t, hipStream_t);
+    const void *(*coop_ptr)();
+    size_t coop_bytes;  // LDS bytes of the cooperative kernel beyond the tables
     hipError_t (*alg)(const AlgParams &, size_t, hipStream_t);
     const void *(*search_ptr)();
     int tmax;
@@ -23,6 +26,7 @@ size_t fast_wave_bytes();
 // Picks the (m, TMAX) instantiation for runtime t (smallest TMAX >= t).
 bool select_kernels(int m, int t, KernelSet *out);
 hipError_t launch_search(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s);
+constexpr int kCoopThreads = 1024;
 hipError_t launch_alg(const KernelSet &k, const AlgParams &p, size_t lds, hipStream_t s);
 hipError_t launch_count(int n, const uint8_t *tx, const uint8_t *res, const bchk_stats *st,
                         uint32_t B, uint64_t *out6, hipStream_t s);

@@ -15,10 +15,30 @@ pytestmark = pytest.mark.gpu
 _ctx = {}
 
 
-def dec(m, t, J=-1, fast=True):
-    key = (m, t, J, fast)
+# execution paths, all of which must give the reference's results:
+#   "fast+exact+coop"  default: lane-per-codeword fast path, wave-per-codeword exact kernel,
+#                      workgroup-cooperative kernel after 4 chunks
+#   "exact-only"       no fast path, no cooperative hand-off (one wave per codeword)
+#   "coop-heavy"       cooperative hand-off after the first chunk
+PATHS = {"fast+exact+coop": (True, None), "exact-only": (False, "0"), "coop-heavy": (True, "1")}
+
+
+def dec(m, t, J=-1, fast=True, path=None):
+    if path is not None:
+        fast, limit = PATHS[path]
+    else:
+        limit = None
+    key = (m, t, J, fast, limit)
     if key not in _ctx:
-        d = load().KanekoKernelProcessor(m, t, J=J)
+        old = os.environ.pop("BCHK_CHUNK_LIMIT", None)
+        if limit is not None:
+            os.environ["BCHK_CHUNK_LIMIT"] = limit
+        try:
+            d = load().KanekoKernelProcessor(m, t, J=J)
+        finally:
+            os.environ.pop("BCHK_CHUNK_LIMIT", None)
+            if old is not None:
+                os.environ["BCHK_CHUNK_LIMIT"] = old
         d.set_fast_path(fast)
         _ctx[key] = d
     return _ctx[key]
@@ -67,20 +87,21 @@ def test_alg_decoder_from_stored_syndromes():
     np.testing.assert_array_equal(a1[ok1] ^ words[ok1], a2[ok2])
 
 
-@pytest.mark.parametrize("fast", [True, False], ids=["fast+exact", "exact-only"])
+@pytest.mark.parametrize("exec_path", list(PATHS))
 @pytest.mark.parametrize("path", vector_files(), ids=os.path.basename)
-def test_kaneko_matches_reference_vectors(path, fast):
+def test_kaneko_matches_reference_vectors(path, exec_path):
     v = load_vectors(path)
-    d = dec(v.m, v.t, fast=fast)
+    d = dec(v.m, v.t, path=exec_path)
     assert (d.n, d.k) == (v.n, v.k)
     np.testing.assert_array_equal(d.g, v.g)
     res, l0, st = d.decode(v.y)
     check_against(v.res, v.l0, v.decodes, v.cmp, v.sums, v.accepted, res, l0, st)
 
 
-def test_kaneko_infile_known_answer():
+@pytest.mark.parametrize("exec_path", list(PATHS))
+def test_kaneko_infile_known_answer(exec_path):
     v = load_vectors(os.path.join(GOLD, "infile_m6t6.txt"))
-    res, l0, st = dec(6, 6).decode(v.y)
+    res, l0, st = dec(6, 6, path=exec_path).decode(v.y)
     np.testing.assert_array_equal(res[0], v.res[0])
     assert l0[0] == v.l0[0]
     assert st["decodes"][0] == 524287
@@ -96,14 +117,14 @@ def test_word_variant_infile_known_answer():
     assert st["decodes"][0] == 524288
 
 
-@pytest.mark.parametrize("fast", [True, False], ids=["fast+exact", "exact-only"])
+@pytest.mark.parametrize("exec_path", list(PATHS))
 @pytest.mark.parametrize("m,t,snr,B", [(6, 6, 3.0, 64), (6, 6, 4.0, 256), (6, 6, 5.0, 512),
                                        (6, 6, 6.0, 2048), (5, 3, 1.0, 256), (5, 3, 5.0, 2048),
                                        (4, 2, 0.0, 512), (4, 2, 6.0, 2048), (8, 15, 5.0, 32)])
-def test_kaneko_j15_matches_oracle(m, t, snr, B, fast):
+def test_kaneko_j15_matches_oracle(m, t, snr, B, exec_path):
     o = Oracle(m, t)
     _, y = o.stream(101, B, snr)
-    res, l0, st = dec(m, t, J=15, fast=fast).decode(y)
+    res, l0, st = dec(m, t, J=15, path=exec_path).decode(y)
     r2, l2, s2, a2 = o.kaneko_batch(y, J=15)
     check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, res, l0, st)
 
@@ -200,12 +221,25 @@ def test_fast_path_handles_adversarial_rows():
     assert st["flags"][0] & F.F_TIE
 
 
-def test_fast_and_exact_paths_agree_at_scale():
-    d_fast, d_exact = dec(6, 6, J=15, fast=True), dec(6, 6, J=15, fast=False)
-    for snr in (4.0, 6.0):
-        _, y, _ = d_fast.generate(snr, 1 << 16, seed=31)
-        a = d_fast.decode(y)
-        b = d_exact.decode(y)
-        np.testing.assert_array_equal(a[0], b[0])
-        np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
-        np.testing.assert_array_equal(a[2], b[2])
+def test_execution_paths_agree_at_scale():
+    ds = [dec(6, 6, J=15, path=p) for p in PATHS]
+    for snr in (4.0, 5.0, 6.0):
+        _, y, _ = ds[0].generate(snr, 1 << 16, seed=31)
+        a = ds[0].decode(y)
+        for d in ds[1:]:
+            b = d.decode(y)
+            np.testing.assert_array_equal(a[0], b[0])
+            np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+            np.testing.assert_array_equal(a[2], b[2])
+
+
+def test_path_counts_and_profile_report_each_stage():
+    d = dec(6, 6, J=15)
+    _, y, _ = d.generate(4.0, 1 << 14, seed=5)
+    d.profile(True)
+    d.decode(y)
+    ms, calls = d.profile_read()
+    d.profile(False)
+    to_exact, to_coop = d.path_counts()
+    assert calls == 1 and len(ms) == 3 and ms[0] > 0 and ms[1] > 0
+    assert 0 < to_exact < (1 << 14) and 0 < to_coop <= to_exact
