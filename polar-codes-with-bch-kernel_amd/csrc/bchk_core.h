@@ -55,6 +55,16 @@ __device__ __forceinline__ int xcc_id() {
     return (int)(v & 7u);
 }
 
+// alpha^(la + lb) with log(0) = ZL = 2n-1: the sum is clamped to ZL so the exp table has
+// 2n entries (exp[2n-1] = 0) -- at most 32 dwords for n <= 63, one per LDS bank, so
+// byte lookups from 32 lanes never conflict.
+template <int M>
+__device__ __forceinline__ uint32_t gf_exp2(const uint8_t *ex, int la, int lb) {
+    constexpr int ZL = 2 * ((1 << M) - 1) - 1;
+    const int s = la + lb;
+    return ex[s < ZL ? s : ZL];
+}
+
 template <int NW>
 __device__ __forceinline__ void mask_set(Mask<NW> &m, int p) {
 #pragma unroll
@@ -106,13 +116,13 @@ __device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
             for (int i = 0; i <= TMAX; ++i) lC[i] = lg[C[i]];
             uint32_t d = 0;
 #pragma unroll
-            for (int i = 0; i <= (r < TMAX ? r : TMAX); ++i) d ^= ex[lC[i] + lS[r - i]];
+            for (int i = 0; i <= (r < TMAX ? r : TMAX); ++i) d ^= gf_exp2<M>(ex, lC[i], lS[r - i]);
             const int ld = lg[d];
             const bool chg = (d != 0u) && (2 * L <= r);
 #pragma unroll
             for (int i = TMAX; i >= 0; --i) {
-                const uint32_t g = ex[lgam + lC[i]];
-                C[i] = i ? (g ^ ex[ld + lB[i - 1]]) : g;
+                const uint32_t g = gf_exp2<M>(ex, lgam, lC[i]);
+                C[i] = i ? (g ^ gf_exp2<M>(ex, ld, lB[i - 1])) : g;
             }
             // B <- C_old (length change) or x*B; then x*B for the skipped odd step
 #pragma unroll

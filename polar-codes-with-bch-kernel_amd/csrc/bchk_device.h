@@ -13,7 +13,8 @@ constexpr int kWaveSize = 64;
 constexpr int kWavesPerBlock = 4;
 
 // Per-code lookup tables, one device blob, copied into LDS by every workgroup.
-//   exp8 [4n]        alpha^i for i < 2n-1, 0 above (so log(0) = 2n-1 sums to 0)
+//   exp8 [2n]        alpha^i for i < 2n-1, exp8[2n-1] = 0 (log sums are clamped to
+//                    2n-1 = log(0), bchk_core.h gf_exp2)
 //   log16[2^m]       log_alpha(v); log16[0] = 2n-1
 //   col  [n][W]      odd-syndrome column of position p: byte j of word j/4 =
 //                    alpha^((2j+1) p mod n), j < t   (Decoder::alterSyndromPoly :210-230)

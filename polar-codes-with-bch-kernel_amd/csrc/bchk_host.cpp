@@ -117,7 +117,7 @@ std::vector<uint8_t> make_tables(const Field &f, int t, TableDesc *td) {
     auto align16 = [](size_t v) { return (v + 15) & ~size_t(15); };
     size_t off = 0;
     td->off_exp = (uint32_t)off;
-    off = align16(off + 4 * n);
+    off = align16(off + 2 * n);
     td->off_log = (uint32_t)off;
     off = align16(off + 2 * (size_t(1) << m));
     td->off_col = (uint32_t)off;
@@ -129,7 +129,7 @@ std::vector<uint8_t> make_tables(const Field &f, int t, TableDesc *td) {
     td->EW = EW;
     std::vector<uint8_t> blob(off, 0);
     uint8_t *ex = blob.data() + td->off_exp;
-    for (int i = 0; i < 2 * n - 1; ++i) ex[i] = (uint8_t)f.alog[i % n];
+    for (int i = 0; i < 2 * n - 1; ++i) ex[i] = (uint8_t)f.alog[i % n];  // ex[2n-1] = 0
     uint16_t *lg = reinterpret_cast<uint16_t *>(blob.data() + td->off_log);
     lg[0] = (uint16_t)(2 * n - 1);
     for (int v = 1; v <= n; ++v) lg[v] = (uint16_t)f.log[v];

@@ -336,24 +336,26 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         int m;
         double l;
         const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, diff, m, l);
-        uint64_t okm = ballot(ok && base + (uint64_t)lane < S.bound);
+        const bool live = ok && base + (uint64_t)lane < S.bound;
+        const uint64_t okm = ballot(live);
         if (base == 0 && !(okm & 1ull)) S.firstOK = false;  // :371
-        while (okm) {
-            const int L = (int)__builtin_ctzll(okm);
-            okm &= okm - 1;
+        // Only improvements (l < l0) change the state: m0 at an improvement is the fixed
+        // i = 0 value or, once i = 0 has failed, the improving candidate's own m (:374), and
+        // l0 only decreases, so successes with l >= l0 can be skipped wholesale.
+        uint64_t imp = ballot(live && l < S.l0);
+        while (imp) {
+            const int L = (int)__builtin_ctzll(imp);
             const uint64_t ii = base + (uint64_t)L;
             if (ii >= S.bound) break;
             const double lL = rdlf(l, L);
             const int mL = (int)rdl((uint32_t)m, L);
-            if (!(lL < S.l0)) {  // not an improvement: only the m0 update (:374)
-                if (ii == 0 || !S.firstOK) S.m0 = mL;
-                continue;
-            }
             Mask<NW> d;
 #pragma unroll
             for (int s = 0; s < NW; ++s) d.w[s] = rdl64(diff.w[s], L);
             accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
             if (S.done) break;
+            // l0 dropped: re-filter the later lanes of this chunk
+            imp = ballot(live && l < S.l0) & ~((2ull << L) - 1ull);
         }
         if (S.done) break;
     }
@@ -472,24 +474,24 @@ kaneko_coop_kernel(SearchParams p) {
                         S.done = true;
                         break;
                     }
-                    uint64_t m = okm_l[w];
-                    if (bw == 0 && !(m & 1ull)) S.firstOK = false;  // :371
-                    while (m) {
-                        const int L = (int)__builtin_ctzll(m);
-                        m &= m - 1;
+                    const uint64_t okw = okm_l[w];
+                    if (bw == 0 && !(okw & 1ull)) S.firstOK = false;  // :371
+                    // successes of wave w: only improvements are visited (see search_codeword)
+                    const bool livew = (okw >> lane) & 1ull;
+                    const double lw = livew ? l_l[w * 64 + lane] : 0.0;
+                    uint64_t imp = ballot(livew && lw < S.l0);
+                    while (imp) {
+                        const int L = (int)__builtin_ctzll(imp);
                         const uint64_t ii = bw + (uint64_t)L;
                         if (ii >= S.bound) break;
-                        const double lL = l_l[w * 64 + L];
+                        const double lL = rdlf(lw, L);
                         const int mL = (int)m_l[w * 64 + L];
-                        if (!(lL < S.l0)) {  // not an improvement: only the m0 update (:374)
-                            if (ii == 0 || !S.firstOK) S.m0 = mL;
-                            continue;
-                        }
                         Mask<NW> d;
 #pragma unroll
                         for (int s = 0; s < NW; ++s) d.w[s] = diff_l[(w * 64 + L) * NW + s];
                         accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
                         if (S.done) break;
+                        imp = ballot(livew && lw < S.l0) & ~((2ull << L) - 1ull);
                     }
                 }
                 if (lane == 0) { ctl[0] = S.bound; ctl[1] = S.done ? 1u : 0u; }
