@@ -19,7 +19,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libbchk.so")
+# BCHK_LIB selects another build of the same ABI (e.g. lib/libbchk_diag.so)
+LIB_PATH = os.environ.get("BCHK_LIB") or os.path.join(PKG_DIR, "lib", "libbchk.so")
 
 BCHK_J_SHIPPED = -1
 VARIANT_ANSWER, VARIANT_WORD = 0, 1

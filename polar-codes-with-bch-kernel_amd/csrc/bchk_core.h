@@ -114,13 +114,17 @@ __device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
             int lC[TMAX + 1];
 #pragma unroll
             for (int i = 0; i <= TMAX; ++i) lC[i] = lg[C[i]];
+            // before step k, deg C <= L <= 2k-1; after it, deg C <= 2k+1 (terms beyond are
+            // zero whenever the final L <= t, the only case that can succeed)
             uint32_t d = 0;
 #pragma unroll
-            for (int i = 0; i <= (r < TMAX ? r : TMAX); ++i) d ^= gf_exp2<M>(ex, lC[i], lS[r - i]);
+            for (int i = 0; i <= (2 * k - 1 > 0 ? (2 * k - 1 < TMAX ? 2 * k - 1 : TMAX) : 0); ++i)
+                d ^= gf_exp2<M>(ex, lC[i], lS[r - i]);
             const int ld = lg[d];
             const bool chg = (d != 0u) && (2 * L <= r);
 #pragma unroll
             for (int i = TMAX; i >= 0; --i) {
+                if (i > 2 * k + 1) { C[i] = 0u; continue; }
                 const uint32_t g = gf_exp2<M>(ex, lgam, lC[i]);
                 C[i] = i ? (g ^ gf_exp2<M>(ex, ld, lB[i - 1])) : g;
             }
@@ -189,6 +193,146 @@ __device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
         ok = ok && (cnt == deg);
     }
     return ok;
+}
+
+// ---------------------------------------------------------------------------
+// GF(2^m) on the VALU, m <= 6, no tables: an element is kept "spread", bit b at bit 3b.
+// A 24-bit integer multiply of two spread elements is their carry-less product (every
+// 3-bit slot sums at most m <= 6 terms, so slots never carry into each other; the slot's
+// low bit is the XOR), then x^m = q(x) folds the high slots back. ~5 VALU per product.
+template <int M>
+struct Spread {
+    static constexpr unsigned kPrim[9] = {0, 3, 7, 11, 19, 37, 67, 137, 285};  // main.cpp:14
+    static constexpr uint32_t Q = kPrim[M] ^ (1u << M);
+    static constexpr uint32_t mask_slots(int n) {
+        uint32_t v = 0;
+        for (int k = 0; k < n; ++k) v |= 1u << (3 * k);
+        return v;
+    }
+    static constexpr uint32_t ELEM = mask_slots(M);
+    static constexpr uint32_t PROD = mask_slots(2 * M - 1);
+    static constexpr int deg_q() {
+        int d = 0;
+        for (int b = 0; b < M; ++b)
+            if ((Q >> b) & 1u) d = b;
+        return d;
+    }
+    // folds needed: after one fold the top slot is (m-2) + deg q
+    static constexpr int FOLDS = (M - 2) + deg_q() < M ? 1 : 2;
+};
+
+template <int M>
+__device__ __forceinline__ uint32_t sp_mul(uint32_t a, uint32_t b) {
+    static_assert(M <= 6, "spread GF arithmetic needs m <= 6");
+    uint32_t r = __umul24(a, b) & Spread<M>::PROD;
+#pragma unroll
+    for (int f = 0; f < Spread<M>::FOLDS; ++f) {
+        const uint32_t h = r >> (3 * M);
+        r &= Spread<M>::ELEM;
+#pragma unroll
+        for (int b = 0; b < M; ++b)
+            if ((Spread<M>::Q >> b) & 1u) r ^= h << (3 * b);
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t sp_from(uint32_t v) {  // 6-bit element -> spread
+    v &= 0x3Fu;
+    v = (v | (v << 8)) & 0x0000F00Fu;
+    v = (v | (v << 4)) & 0x000C30C3u;
+    v = (v | (v << 2)) & 0x00009249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t sp_to(uint32_t v) {  // spread -> 6-bit element
+    v &= 0x00009249u;
+    v = (v | (v >> 2)) & 0x000C30C3u;
+    v = (v | (v >> 4)) & 0x0000F00Fu;
+    v = (v | (v >> 8)) & 0x3Fu;
+    return v;
+}
+
+// Same decision as alg_core (inversionless binary BM + Chien table), with BM on the VALU.
+template <int M, int TMAX>
+__device__ __forceinline__ bool alg_core_valu(const uint64_t *__restrict__ chien, const uint32_t *Sw,
+                                              int t, Mask<1> &E) {
+    constexpr int N = (1 << M) - 1;
+    static_assert(N <= 63, "m <= 6");
+    uint32_t S[2 * TMAX];  // S[j-1] = S_j, spread
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) S[2 * j] = sp_from((Sw[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+#pragma unroll
+    for (int e = 2; e <= 2 * TMAX - 1; e += 2) S[e - 1] = sp_mul<M>(S[e / 2 - 1], S[e / 2 - 1]);
+    uint32_t C[TMAX + 1], B[TMAX + 1];
+#pragma unroll
+    for (int i = 0; i <= TMAX; ++i) { C[i] = i ? 0u : 1u; B[i] = i ? 0u : 1u; }
+    uint32_t gam = 1;
+    int L = 0;
+#pragma unroll
+    for (int k = 0; k < TMAX; ++k) {
+        if (k < t) {
+            const int r = 2 * k;
+            uint32_t d = 0;
+#pragma unroll
+            for (int i = 0; i <= (2 * k - 1 > 0 ? (2 * k - 1 < TMAX ? 2 * k - 1 : TMAX) : 0); ++i)
+                d ^= sp_mul<M>(C[i], S[r - i]);
+            const bool chg = (d != 0u) && (2 * L <= r);
+            uint32_t Cn[TMAX + 1];
+#pragma unroll
+            for (int i = 0; i <= TMAX; ++i) {
+                if (i > 2 * k + 1) { Cn[i] = 0u; continue; }
+                const uint32_t g = sp_mul<M>(gam, C[i]);
+                Cn[i] = i ? (g ^ sp_mul<M>(d, B[i - 1])) : g;
+            }
+#pragma unroll
+            for (int i = TMAX; i >= 0; --i) {
+                const uint32_t sh = i ? B[i - 1] : 0u;
+                B[i] = chg ? C[i] : sh;
+            }
+#pragma unroll
+            for (int i = TMAX; i >= 1; --i) B[i] = B[i - 1];
+            B[0] = 0u;
+            L = chg ? r + 1 - L : L;
+            gam = chg ? d : gam;
+#pragma unroll
+            for (int i = 0; i <= TMAX; ++i) C[i] = Cn[i];
+        }
+    }
+    int deg = 0;
+#pragma unroll
+    for (int i = 1; i <= TMAX; ++i) deg = C[i] ? i : deg;
+    bool ok = (L <= t) && (deg >= 1);
+    constexpr int EW = (M + 1) & ~1;
+    uint64_t pl[EW];
+#pragma unroll
+    for (int w = 0; w < EW; ++w) pl[w] = 0;
+#pragma unroll
+    for (int j = 0; j <= TMAX; ++j) {
+        if (j <= t) {
+            const uint64_t *row = chien + (size_t)((j << M) + (int)sp_to(C[j])) * EW;
+#pragma unroll
+            for (int w = 0; w < EW; ++w) pl[w] ^= row[w];
+        }
+    }
+    uint64_t any = 0;
+#pragma unroll
+    for (int b = 0; b < M; ++b) any |= pl[b];
+    const uint64_t zero = ~any & ((1ull << N) - 1ull);
+    ok = ok && (__popcll(zero) == deg);
+    uint64_t e = __builtin_bitreverse64(zero) >> (63 - N);
+    if ((e >> N) & 1ull) e = (e & ((1ull << N) - 1ull)) | 1ull;
+    E.w[0] = e;
+    return ok;
+}
+
+// The decoder a kernel uses: VALU BM for m <= 6 unless BCHK_GF_LDS is defined.
+template <int M, int TMAX>
+__device__ __forceinline__ bool alg_decode_word(const uint8_t *ex, const uint16_t *lg,
+                                                const uint64_t *chien, const uint32_t *Sw, int t,
+                                                Mask<Geo<M>::NW> &E) {
+#ifndef BCHK_GF_LDS
+    if constexpr (M <= 6) return alg_core_valu<M, TMAX>(chien, Sw, t, E);
+    else
+#endif
+        return alg_core<M, TMAX>(ex, lg, chien, Sw, t, E);
 }
 
 __device__ __forceinline__ void load_tables(uint8_t *dst, const uint8_t *src, uint32_t bytes) {

@@ -52,6 +52,8 @@ struct SearchParams {
     uint32_t *heavy_tail;
     uint32_t *heavy_head;
     uint32_t chunk_limit;
+    // diagnostic builds only (-DBCHK_DIAG): per heavy-queue item, 8 u64 timing counters
+    unsigned long long *diag;
     int32_t t;
     int32_t J;             // < 0: shipped
     int32_t variant;       // BCHK_VARIANT_*

@@ -188,7 +188,7 @@ struct bchk_ctx {
     size_t lds_fast = 0, lds_coop = 0;
     int grid_coop = 0;
     uint32_t chunk_limit = 4;
-    DevBuf queue, heavy, ctrl;  // work queues + control words (one 128-B line each)
+    DevBuf queue, heavy, ctrl, diag;  // work queues + control words (one 128-B line each)
     uint8_t *d_tables = nullptr;
     hipStream_t stream = nullptr;
     size_t lds = 0, lds_alg = 0;
@@ -240,6 +240,11 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     p.heavy_tail = c->chunk_limit ? ctrl + kHeavyTail : nullptr;
     p.heavy_head = ctrl + kHeavyHead;
     p.chunk_limit = c->chunk_limit;
+#ifdef BCHK_DIAG
+    if (!c->diag.p) (void)c->diag.ensure(size_t(1) << 24);
+    (void)hipMemsetAsync(c->diag.p, 0, size_t(1) << 24, s);
+    p.diag = (unsigned long long *)c->diag.p;
+#endif
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (c->profile) {
         for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
@@ -633,6 +638,17 @@ int bchk_path_counts(bchk_ctx *c, uint64_t *to_exact, uint64_t *to_coop) {
     if (to_coop) *to_coop = v[1];
     return 0;
 }
+
+#ifdef BCHK_DIAG
+// diagnostic builds: copy the cooperative kernel's per-item stamps (8 u64 each)
+int bchk_diag_read(bchk_ctx *c, uint64_t *out, size_t items) {
+    if (!c || !out) return fail(BCHK_EINVAL, "NULL argument");
+    if (!c->diag.p) return fail(BCHK_EINVAL, "not a diagnostic build");
+    const size_t bytes = std::min(items * 64, c->diag.cap);
+    HIP_TRY(hipMemcpy(out, c->diag.p, bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+#endif
 
 int bchk_set_fast_path(bchk_ctx *c, int enable) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");

@@ -163,7 +163,7 @@ __device__ __forceinline__ bool decode_chunk(const Prep<M, TMAX> &P, uint64_t ba
         mask_set<NW>(Pm, pb);
     }
     Mask<NW> E;
-    const bool ok = alg_core<M, TMAX>(ex, lg, chien, Sw, t, E);
+    const bool ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, t, E);
 #pragma unroll
     for (int s = 0; s < NW; ++s) diff.w[s] = Pm.w[s] ^ E.w[s];
     m = 0;
@@ -438,8 +438,18 @@ kaneko_coop_kernel(SearchParams p) {
         const uint32_t item = (uint32_t)ctl[2];
         if (item >= total) return;
         const uint32_t cw = p.heavy_queue[item];
+#ifdef BCHK_DIAG
+        // stamps (wave 0): [0] prep, [1] own decodes, [2] wait for the other waves,
+        // [3] ordered acceptance, [4] rounds, [5] improvements, [6] total
+        unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
         Prep<M, TMAX> P;  // every wave builds the same prep (its own LDS slice)
         prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+#ifdef BCHK_DIAG
+        unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+        dg[0] = t_prev - t_start;
+#endif
         SearchState<NW> S;
         init_state<M>(S, p.variant);
         if (threadIdx.x == 0) { ctl[0] = S.bound; ctl[1] = 0; }
@@ -463,7 +473,17 @@ kaneko_coop_kernel(SearchParams p) {
                 }
             }
             if (lane == 0) okm_l[wid] = okm;
+#ifdef BCHK_DIAG
+            const unsigned long long t_dec = __builtin_amdgcn_s_memtime();
+#endif
             __syncthreads();
+#ifdef BCHK_DIAG
+            const unsigned long long t_bar = __builtin_amdgcn_s_memtime();
+            dg[1] += t_dec - t_prev;
+            dg[2] += t_bar - t_dec;
+            dg[4] += 1;
+            const uint64_t impr0 = S.impr;
+#endif
             if (wid == 0) {
                 for (int w = 0; w < kCoopWaves && !S.done; ++w) {
                     const uint64_t bw = rbase + 64 * (uint64_t)w;
@@ -496,8 +516,19 @@ kaneko_coop_kernel(SearchParams p) {
                 }
                 if (lane == 0) { ctl[0] = S.bound; ctl[1] = S.done ? 1u : 0u; }
             }
+#ifdef BCHK_DIAG
+            t_prev = __builtin_amdgcn_s_memtime();
+            dg[3] += t_prev - t_bar;
+            dg[5] += S.impr - impr0;
+#endif
         }
         if (wid == 0) write_outputs<M, TMAX>(S, P, p, cw, lane);
+#ifdef BCHK_DIAG
+        dg[6] = __builtin_amdgcn_s_memtime() - t_start;
+        dg[7] = cw;
+        if (p.diag && threadIdx.x == 0)
+            for (int q = 0; q < 8; ++q) p.diag[(size_t)item * 8 + q] = dg[q];
+#endif
         (void)N;
     }
 }
@@ -532,7 +563,7 @@ __global__ void __launch_bounds__(256) alg_decode_kernel(AlgParams p) {
         }
     }
     Mask<NW> E;
-    const bool ok = alg_core<M, TMAX>(ex, lg, chien, Sw, p.t, E);
+    const bool ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, p.t, E);
     if (!live) return;
     p.ok[idx] = ok ? 1 : 0;
     if (ok)

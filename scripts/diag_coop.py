@@ -1,0 +1,28 @@
+"""Diagnostic (libbchk_diag.so): per heavy codeword, where the cooperative kernel's cycles go."""
+import ctypes as C
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["BCHK_LIB"] = os.path.join(REPO, "polar-codes-with-bch-kernel_amd", "lib", "libbchk_diag.so")
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+from bchk_pkg import load  # noqa: E402
+
+bchk = load()
+L = bchk.lib()
+L.bchk_diag_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+d = bchk.KanekoKernelProcessor(6, 6, J=15)
+tx, y, _ = d.generate(5.0, 1 << 20, seed=1)
+res, l0, st = d.decode(y)
+_, n_coop = d.path_counts()
+buf = np.zeros((n_coop, 8), np.uint64)
+assert L.bchk_diag_read(d.handle, buf.ctypes.data, n_coop) == 0
+dec = st["decodes"][buf[:, 7].astype(np.int64)]
+names = ["prep", "own_decode", "wait_others", "accept", "rounds", "improvements", "total"]
+out = {"n": int(n_coop), "sum": {k: int(buf[:, i].sum()) for i, k in enumerate(names)}}
+top = np.argsort(-buf[:, 6].astype(np.int64))[:8]
+out["top"] = [{**{k: int(buf[j, i]) for i, k in enumerate(names)}, "decodes": int(dec[j])} for j in top]
+print(json.dumps(out))
