@@ -67,6 +67,18 @@ kaneko_fast_kernel(SearchParams p) {
     const double s2 = p.s2;
     const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
 
+#ifdef BCHK_DIAG
+    // stamps: [0] stage+keys, [1] sort, [2] S0, [3] decode i=0 + accept, [4] i=1, [5] outputs
+    unsigned long long dg[6], tp = __builtin_amdgcn_s_memtime();
+#define BCHK_STAMP(i)                                          \
+    {                                                          \
+        const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
+        dg[i] = tn - tp;                                       \
+        tp = tn;                                               \
+    }
+#else
+#define BCHK_STAMP(i)
+#endif
     // ---- stage rows, build keys and the hard decision yH = (2y/s2 > 0) (:336-342)
     const uint32_t last_row = p.count - 1u - cw0;  // rows past the batch end clamp (unused)
     uint32_t key[64];
@@ -104,6 +116,7 @@ kaneko_fast_kernel(SearchParams p) {
     }
 #pragma unroll
     for (int q = N; q < 64; ++q) key[q] = 0xFFFFFFFFu;
+    BCHK_STAMP(0)
 
     // ---- bitonic sort of the 64 keys, ascending
 #pragma unroll
@@ -123,6 +136,7 @@ kaneko_fast_kernel(SearchParams p) {
         }
     }
 
+    BCHK_STAMP(1)
     // ---- sorted prefix. Distinct 26-bit prefixes imply |y| values >= 2^-21 apart
     // (relative), so their alphas are strictly ordered exactly as the reference's
     // (|alpha|, position) order; any equal prefix up to the boundary pair (KMAX, KMAX+1)
@@ -144,6 +158,7 @@ kaneko_fast_kernel(SearchParams p) {
         for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w] & on;
     }
 
+    BCHK_STAMP(2)
     // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`.
     auto accept = [&](uint64_t diff, double &l, bool &ret) {
         const int m = __popcll(diff);
@@ -176,6 +191,7 @@ kaneko_fast_kernel(SearchParams p) {
         accept(E.w[0], l, ret);
         if (ret) { state = 1; best = E.w[0]; l0 = l; }
     }
+    BCHK_STAMP(3)
     // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371)
     const bool need1 = live && !bad && !ok0;
     if (ballot(need1)) {
@@ -193,6 +209,7 @@ kaneko_fast_kernel(SearchParams p) {
         }
     }
 
+    BCHK_STAMP(4)
     // ---- outputs: resolved rows through LDS, one coalesced 64-row block per wave
     const bool resolved = live && state != 0;
     uint8_t *out = reinterpret_cast<uint8_t *>(stage);
@@ -231,6 +248,12 @@ kaneko_fast_kernel(SearchParams p) {
             p.st[cw] = st;
         }
     }
+    BCHK_STAMP(5)
+#ifdef BCHK_DIAG
+    if (p.diag && lane == 0)
+        for (int q = 0; q < 6; ++q) p.diag[(size_t)(cw0 / 64) * 8 + q] = dg[q];
+#endif
+#undef BCHK_STAMP
     // ---- everything else goes to the exact wave-per-codeword path
     const bool unres = live && state == 0;
     const uint64_t um = ballot(unres);

@@ -245,6 +245,7 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     (void)hipMemsetAsync(c->diag.p, 0, size_t(1) << 24, s);
     p.diag = (unsigned long long *)c->diag.p;
 #endif
+
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     if (c->profile) {
         for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
@@ -254,6 +255,9 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     if (c->fast && c->use_fast) {
         if ((rc = c->queue.ensure(B * sizeof(uint32_t)))) return rc;
         SearchParams f = p;
+#ifdef BCHK_DIAG
+        f.diag = p.diag + (size_t(1) << 20);  // fast-kernel stamps: second half of the buffer
+#endif
         f.qtail = ctrl;
         f.queue_out = (uint32_t *)c->queue.p;
         HIP_TRY(c->fast(f, c->lds_fast, s));

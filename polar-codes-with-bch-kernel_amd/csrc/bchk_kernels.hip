@@ -468,9 +468,9 @@ kaneko_coop_kernel(SearchParams p) {
                 if (ok) {
 #pragma unroll
                     for (int s = 0; s < NW; ++s) diff_l[(wid * 64 + lane) * NW + s] = diff.w[s];
-                    l_l[wid * 64 + lane] = l;
                     m_l[wid * 64 + lane] = (uint32_t)m;
                 }
+                l_l[wid * 64 + lane] = l;
             }
             if (lane == 0) okm_l[wid] = okm;
 #ifdef BCHK_DIAG
@@ -485,33 +485,59 @@ kaneko_coop_kernel(SearchParams p) {
             const uint64_t impr0 = S.impr;
 #endif
             if (wid == 0) {
-                for (int w = 0; w < kCoopWaves && !S.done; ++w) {
-                    const uint64_t bw = rbase + 64 * (uint64_t)w;
-                    if (bw >= S.bound) { S.i_end = S.bound; S.done = true; break; }
-                    if (p.max_decodes && bw >= p.max_decodes) {
-                        S.i_end = bw;
+                // All 16 waves' success masks and calcL values in one batch of LDS reads;
+                // the next improvement (l < l0, in pattern order) is found with 16 ballots
+                // from registers, and accept_success runs once per improvement (rare).
+                uint64_t okw[kCoopWaves];
+                double lw[kCoopWaves];
+#pragma unroll
+                for (int w = 0; w < kCoopWaves; ++w) {
+                    okw[w] = okm_l[w];
+                    lw[w] = l_l[w * 64 + lane];
+                }
+                if (rbase == 0 && !(okw[0] & 1ull)) S.firstOK = false;  // :371
+                // patterns this round may run to: the loop bound, or the safety cap rounded
+                // up to its 64-pattern chunk (as the single-wave kernel applies it)
+                const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63) & ~63ull) : ~0ull;
+                uint64_t stop = S.bound < capc ? S.bound : capc;
+                int from = 0;  // linear index (64 w + lane) to search from
+                for (;;) {
+                    int fw = -1, fl = 0;
+#pragma unroll
+                    for (int w = kCoopWaves - 1; w >= 0; --w) {
+                        uint64_t im = ballot(((okw[w] >> lane) & 1ull) && lw[w] < S.l0);
+                        const int lo = from - 64 * w;  // lanes below `from` are done
+                        im = lo <= 0 ? im : (lo >= 64 ? 0ull : (im & ~((1ull << lo) - 1ull)));
+                        if (im) { fw = w; fl = (int)__builtin_ctzll(im); }
+                    }
+                    if (fw < 0) break;
+                    const uint64_t ii = rbase + 64 * (uint64_t)fw + (uint64_t)fl;
+                    if (ii >= stop) break;
+                    double lsel = 0.0;
+#pragma unroll
+                    for (int w = 0; w < kCoopWaves; ++w) lsel = (w == fw) ? lw[w] : lsel;
+                    const double lL = rdlf(lsel, fl);
+                    const int mL = (int)m_l[fw * 64 + fl];
+                    Mask<NW> d;
+#pragma unroll
+                    for (int s = 0; s < NW; ++s) d.w[s] = diff_l[(fw * 64 + fl) * NW + s];
+                    accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
+                    if (S.done) break;
+                    stop = S.bound < capc ? S.bound : capc;
+                    from = 64 * fw + fl + 1;
+                }
+                // the loop ends in this round when it reaches the bound, or is cut at the
+                // cap; whichever chunk comes first (the bound wins a tie), as the
+                // single-wave kernel decides at its chunk starts
+                if (!S.done) {
+                    const uint64_t rend = rbase + 64 * (uint64_t)kCoopWaves;
+                    const uint64_t nb = (S.bound + 63) & ~63ull;
+                    if (nb <= capc) {
+                        if (S.bound <= rend) { S.i_end = S.bound; S.done = true; }
+                    } else if (capc <= rend) {
+                        S.i_end = capc;
                         S.truncated = true;
                         S.done = true;
-                        break;
-                    }
-                    const uint64_t okw = okm_l[w];
-                    if (bw == 0 && !(okw & 1ull)) S.firstOK = false;  // :371
-                    // successes of wave w: only improvements are visited (see search_codeword)
-                    const bool livew = (okw >> lane) & 1ull;
-                    const double lw = livew ? l_l[w * 64 + lane] : 0.0;
-                    uint64_t imp = ballot(livew && lw < S.l0);
-                    while (imp) {
-                        const int L = (int)__builtin_ctzll(imp);
-                        const uint64_t ii = bw + (uint64_t)L;
-                        if (ii >= S.bound) break;
-                        const double lL = rdlf(lw, L);
-                        const int mL = (int)m_l[w * 64 + L];
-                        Mask<NW> d;
-#pragma unroll
-                        for (int s = 0; s < NW; ++s) d.w[s] = diff_l[(w * 64 + L) * NW + s];
-                        accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
-                        if (S.done) break;
-                        imp = ballot(livew && lw < S.l0) & ~((2ull << L) - 1ull);
                     }
                 }
                 if (lane == 0) { ctl[0] = S.bound; ctl[1] = S.done ? 1u : 0u; }

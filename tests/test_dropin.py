@@ -82,12 +82,29 @@ def test_cli_sweep_csv_is_the_references(binary, m, t, p, e, tmp_path):
 
 
 @pytest.mark.gpu
-def test_cli_sweep_j15_md5(tmp_path):
+@pytest.mark.parametrize("m,t,md5", [
+    (5, 3, "105c77e4bb47a243054121d9c907feae"),
+    # the headline configuration (SURVEY.md §6.4 / BASELINE.md): BCH(63,30,13), J=15,
+    # p=10^6 e=100 -- md5 of the reference binary's CSV as recorded there
+    (6, 6, "e0beb7a4b884a4d0b8393c270827b028")])
+def test_cli_sweep_j15_md5(m, t, md5, tmp_path):
     _need_bins()
-    r = _run(["kaneko", "5", "3", "j15", "1000000", "100"], cwd=tmp_path, env={"BCHK_J": "15"})
+    r = _run(["kaneko", str(m), str(t), "j15", "1000000", "100"], cwd=tmp_path,
+             env={"BCHK_J": "15"})
     assert r.returncode == 0, r.stderr
     csv = open(tmp_path / "j15.csv").read()
-    assert hashlib.md5(csv.encode()).hexdigest() == "105c77e4bb47a243054121d9c907feae"
+    assert hashlib.md5(csv.encode()).hexdigest() == md5
+
+
+@pytest.mark.gpu
+def test_cli_sweep_bch15_shipped_md5(tmp_path):
+    """`kaneko 4 2 x 1000000 1000` with the shipped (uncapped) search: md5 of the reference
+    binary's CSV recorded in SURVEY.md §6.2."""
+    _need_bins()
+    r = _run(["kaneko", "4", "2", "x", "1000000", "1000"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    csv = open(tmp_path / "x.csv").read()
+    assert hashlib.md5(csv.encode()).hexdigest() == "82dcef4a50ad04e68ac2385ebafdcd06"
 
 
 @pytest.mark.gpu

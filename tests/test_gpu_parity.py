@@ -170,14 +170,16 @@ def test_untouched_rows_and_edge_inputs():
     assert r.shape == (0, 63)
 
 
-def test_max_decodes_cap_flags_truncation():
+@pytest.mark.parametrize("exec_path", list(PATHS))
+def test_max_decodes_cap_flags_truncation(exec_path):
     F = load()
     v = load_vectors(os.path.join(GOLD, "infile_m6t6.txt"))
-    d = load().KanekoKernelProcessor(6, 6)
+    d = dec(6, 6, path=exec_path)
     d.set_max_decodes(1000)
     res, l0, st = d.decode(v.y)
+    d.set_max_decodes(0)
     assert st["flags"][0] & F.F_TRUNCATED
-    assert st["decodes"][0] <= 1024
+    assert st["decodes"][0] == 1024  # cut at the first 64-pattern chunk at/after the cap
 
 
 def test_large_batch_sampled_against_oracle_and_deterministic():
