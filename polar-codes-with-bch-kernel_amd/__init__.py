@@ -126,7 +126,13 @@ class KanekoKernelProcessor:
             lib().bchk_destroy(self._h)
             self._h = None
 
-    __del__ = close
+    def __del__(self):
+        # at interpreter shutdown the module globals may already be gone: the process
+        # teardown releases the device memory then
+        try:
+            self.close()
+        except (TypeError, AttributeError):
+            pass
 
     @property
     def handle(self):

@@ -16,8 +16,20 @@ struct Geo {
     static constexpr int N = (1 << M) - 1;
     static constexpr int NW = (N + 63) / 64;    // u64 words per position mask
     static constexpr int ZL = 2 * N - 1;        // log(0) sentinel
-    static constexpr int EW = (M + 1) & ~1;     // Chien row u64 words (16-B aligned)
 };
+
+// Chien map (m <= 6): planes pl[b] ^= T[j][lo][b] ^ T[j][hi][b], value = lo + 8 hi.
+template <int M>
+__device__ __forceinline__ void chien_add(const uint64_t *__restrict__ chien, int j, uint32_t lo,
+                                          uint32_t hi, uint64_t (&pl)[M]) {
+    const uint64_t *tl = chien + (size_t)j * (2 * M * 8);
+#pragma unroll
+    for (int b = 0; b < M; ++b) {
+        uint64_t v = tl[b * 8 + lo];
+        if constexpr (M > 3) v ^= tl[(M + b) * 8 + hi];
+        pl[b] ^= v;
+    }
+}
 
 template <int NW>
 struct Mask {
@@ -148,18 +160,12 @@ __device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
     bool ok = (L <= t) && (deg >= 1);
 
     if constexpr (M <= 6) {
-        constexpr int EW = Geo<M>::EW;
-        uint64_t pl[EW];
+        uint64_t pl[M];
 #pragma unroll
-        for (int w = 0; w < EW; ++w) pl[w] = 0;
+        for (int b = 0; b < M; ++b) pl[b] = 0;
 #pragma unroll
-        for (int j = 0; j <= TMAX; ++j) {
-            if (j <= t) {
-                const uint64_t *row = chien + (size_t)((j << M) + (int)C[j]) * EW;
-#pragma unroll
-                for (int w = 0; w < EW; ++w) pl[w] ^= row[w];
-            }
-        }
+        for (int j = 0; j <= TMAX; ++j)
+            if (j <= t) chien_add<M>(chien, j, C[j] & 7u, C[j] >> 3, pl);
         uint64_t any = 0;
 #pragma unroll
         for (int b = 0; b < M; ++b) any |= pl[b];
@@ -300,16 +306,17 @@ __device__ __forceinline__ bool alg_core_valu(const uint64_t *__restrict__ chien
 #pragma unroll
     for (int i = 1; i <= TMAX; ++i) deg = C[i] ? i : deg;
     bool ok = (L <= t) && (deg >= 1);
-    constexpr int EW = (M + 1) & ~1;
-    uint64_t pl[EW];
+    uint64_t pl[M];
 #pragma unroll
-    for (int w = 0; w < EW; ++w) pl[w] = 0;
+    for (int b = 0; b < M; ++b) pl[b] = 0;
 #pragma unroll
     for (int j = 0; j <= TMAX; ++j) {
         if (j <= t) {
-            const uint64_t *row = chien + (size_t)((j << M) + (int)sp_to(C[j])) * EW;
-#pragma unroll
-            for (int w = 0; w < EW; ++w) pl[w] ^= row[w];
+            // spread bits 0,3,6 (and 9,12,15) gathered into 3-bit indices by one multiply:
+            // x * 21 = x + 4x + 16x puts spread bits 0/3/6 at 4/5/6 with no carries
+            const uint32_t lo = (((C[j] & 0x49u) * 21u) >> 4) & 7u;
+            const uint32_t hi = ((((C[j] >> 9) & 0x49u) * 21u) >> 4) & 7u;
+            chien_add<M>(chien, j, lo, hi, pl);
         }
     }
     uint64_t any = 0;

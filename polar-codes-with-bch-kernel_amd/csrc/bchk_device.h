@@ -18,13 +18,15 @@ constexpr int kWavesPerBlock = 4;
 //   log16[2^m]       log_alpha(v); log16[0] = 2n-1
 //   col  [n][W]      odd-syndrome column of position p: byte j of word j/4 =
 //                    alpha^((2j+1) p mod n), j < t   (Decoder::alterSyndromPoly :210-230)
-//   chien[t+1][2^m][EW] (m <= 6 only) bit-planes of v * alpha^(j k) over k = 0..n-1:
+//   chien[t+1][2][m][8] (m <= 6 only) bit-planes of v * alpha^(j k) over k = 0..n-1:
 //                    the Chien search of Decoder::locatorsAndRoots (:279-296) as a
-//                    GF(2)-linear map, XOR of t+1 table rows.
+//                    GF(2)-linear map. v splits into its low and high 3-bit halves
+//                    (v = lo + 8 hi), each indexing an 8-entry table per (j, plane b):
+//                    rows of 8 u64 = 16 LDS banks, so lanes never conflict.
 struct TableDesc {
     uint32_t off_exp, off_log, off_col, off_chien, bytes;
     int32_t W;   // u32 words per packed odd-syndrome vector
-    int32_t EW;  // u64 words per Chien table row
+    int32_t EW;  // unused (kept for the struct layout)
 };
 
 struct SearchParams {

@@ -9,7 +9,7 @@
 //     builds 32-bit sort keys (26-bit monotone prefix of |y|, 6-bit position) and sorts
 //     them with a 64-key bitonic network in registers;
 //   - distinct prefixes order alpha = |2y/s2| exactly; a prefix tie within the sorted
-//     prefix calcRightSide can touch (3t+3 entries) sends the codeword to the exact slow
+//     prefix calcRightSide can touch (2t+1 entries) sends the codeword to the exact slow
 //     path; the alphas that enter sums are recomputed exactly (IEEE f64 division of the
 //     row's samples, gathered on demand);
 //   - decodes i = 0 and i = 1 run per lane (binary BM + Chien table);
@@ -17,6 +17,8 @@
 // Codewords not resolved here (no early return at i <= 1, or any doubt) are appended to a
 // queue that the wave-per-codeword kernel (bchk_kernels.hip) processes from scratch, so
 // every result is the reference's.
+#include <algorithm>
+
 #include "bchk_core.h"
 #include "bchk_launch.h"
 
@@ -25,6 +27,7 @@ namespace bchk {
 namespace {
 constexpr int kRowD = 9;  // doubles per staged row slice (8 + 1 pad: conflict-free b64)
 constexpr int kSlice = 8;
+constexpr int kFastWaves = 8;  // waves per persistent block
 }  // namespace
 
 // 32-bit sort key: a monotone 26-bit prefix of |y| (5 exponent bits covering
@@ -39,15 +42,18 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t hi, uint32_t lo, int pos) 
     return (pre << 6) | (uint32_t)pos;
 }
 
-// 3 waves per SIMD: the register allocator fits 168 VGPRs (a 12-B spill) instead of 220
-// (2 waves per SIMD); the kernel is latency-bound, so occupancy wins.
+// Blocks of kFastWaves waves, one 64-codeword chunk per wave: the code tables are staged
+// into LDS once per 512 codewords, and two blocks per CU give 4 waves per SIMD (<= 128
+// VGPRs; the kernel is latency-bound, so occupancy wins).
 template <int M, int TMAX>
-__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock, 3)
+__global__ void __launch_bounds__(kWaveSize * kFastWaves, 4)
 kaneko_fast_kernel(SearchParams p) {
     constexpr int N = Geo<M>::N;
     static_assert(N <= 63, "fast path covers n <= 63");
     constexpr int W = (TMAX + 3) / 4;
-    constexpr int KMAX = (3 * TMAX + 2 < N - 1) ? 3 * TMAX + 2 : N - 1;
+    // calcRightSide takes the first border = 2t+1-m agreeing sorted positions; with m0 == m
+    // (both fast-path exits) and m positions disagreeing, they lie within ranks 0..2t.
+    constexpr int KMAX = (2 * TMAX < N - 1) ? 2 * TMAX : N - 1;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
     __syncthreads();
@@ -58,7 +64,7 @@ kaneko_fast_kernel(SearchParams p) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double *stage = reinterpret_cast<double *>(smem + ((p.td.bytes + 15) & ~15u) +
                                                wid * (64 * kRowD * 8));
-    const uint32_t cw0 = (blockIdx.x * kWavesPerBlock + wid) * 64u;
+    const uint32_t cw0 = (blockIdx.x * kFastWaves + wid) * 64u;
     if (cw0 >= p.count) return;
     const uint32_t cw = cw0 + (uint32_t)lane;
     const bool live = cw < p.count;
@@ -79,25 +85,34 @@ kaneko_fast_kernel(SearchParams p) {
 #else
 #define BCHK_STAMP(i)
 #endif
-    // ---- stage rows, build keys and the hard decision yH = (2y/s2 > 0) (:336-342)
+    // ---- stage rows, build keys and the hard decision yH = (2y/s2 > 0) (:336-342).
+    // Slice loads run kAhead slices ahead of the slice being turned into keys, so a wave
+    // waits for one memory round trip instead of one per slice.
     const uint32_t last_row = p.count - 1u - cw0;  // rows past the batch end clamp (unused)
+    constexpr int NS = (N + kSlice - 1) / kSlice;
+    constexpr int kAhead = 2;
     uint32_t key[64];
-    uint64_t yH = 0;
-#pragma unroll
-    for (int c = 0; c < (N + kSlice - 1) / kSlice; ++c) {
-        double v[kSlice];
+    uint32_t yHl = 0, yHh = 0;
+    double v[kAhead + 1][kSlice];
+    auto load_slice = [&](int c, double *dst) {
 #pragma unroll
         for (int it = 0; it < kSlice; ++it) {
             const int flat = it * 64 + lane;
             const uint32_t r = (uint32_t)(flat >> 3);
             const int pos = kSlice * c + (flat & 7);
             const uint32_t rr = r < last_row ? r : last_row;
-            v[it] = p.y[(size_t)(cw0 + rr) * N + (pos < N ? pos : N - 1)];
+            dst[it] = p.y[(size_t)(cw0 + rr) * N + (pos < N ? pos : N - 1)];
         }
+    };
+#pragma unroll
+    for (int c = 0; c < kAhead && c < NS; ++c) load_slice(c, v[c]);
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+        if (c + kAhead < NS) load_slice(c + kAhead, v[(c + kAhead) % (kAhead + 1)]);
 #pragma unroll
         for (int it = 0; it < kSlice; ++it) {
             const int flat = it * 64 + lane;
-            stage[(flat >> 3) * kRowD + (flat & 7)] = v[it];
+            stage[(flat >> 3) * kRowD + (flat & 7)] = v[c % (kAhead + 1)][it];
         }
         wave_sync();
 #pragma unroll
@@ -107,16 +122,30 @@ kaneko_fast_kernel(SearchParams p) {
                 const uint64_t b = (uint64_t)__double_as_longlong(stage[lane * kRowD + k]);
                 const uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
                 key[pos] = sort_key(hi, lo, pos);
-                // y > 0 (sign clear, nonzero); tiny/subnormal y, whose alpha could underflow,
-                // has prefix 0 and is sent to the slow path below
-                yH |= (uint64_t)(((int32_t)hi >= 0) && ((hi | lo) != 0u)) << pos;
+                // y > 0 is the clear sign bit: y = +0 (and tiny/subnormal y, whose alpha
+                // could underflow) has prefix 0 and is sent to the slow path below
+                // sign bits shifted in from the top (no per-position constants)
+                if (pos < 32) yHl = (yHl >> 1) | (hi & 0x80000000u);
+                else yHh = (yHh >> 1) | (hi & 0x80000000u);
             }
         }
         wave_sync();
     }
 #pragma unroll
     for (int q = N; q < 64; ++q) key[q] = 0xFFFFFFFFu;
+    // yHl/yHh hold the sign bits of positions 0..31 / 32..N-1, last position at bit 31
+    if constexpr (N < 32) {
+        yHl >>= 32 - N;
+        yHh = 0;
+    } else if constexpr (N < 64) {
+        yHh >>= 64 - N;
+    }
+    const uint64_t yH = ~(((uint64_t)yHh << 32) | yHl) & ((1ull << N) - 1ull);
     BCHK_STAMP(0)
+#if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 1
+    if (p.l0 && live) p.l0[cw] = (double)(key[5] ^ key[17] ^ key[40] ^ (uint32_t)yH);
+    return;
+#endif
 
     // ---- bitonic sort of the 64 keys, ascending
 #pragma unroll
@@ -137,16 +166,44 @@ kaneko_fast_kernel(SearchParams p) {
     }
 
     BCHK_STAMP(1)
+#if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 2
+    if (p.l0 && live) p.l0[cw] = (double)(key[5] ^ key[17] ^ key[40] ^ (uint32_t)yH);
+    return;
+#endif
     // ---- sorted prefix. Distinct 26-bit prefixes imply |y| values >= 2^-21 apart
     // (relative), so their alphas are strictly ordered exactly as the reference's
-    // (|alpha|, position) order; any equal prefix up to the boundary pair (KMAX, KMAX+1)
-    // sends the codeword to the exact slow path.
+    // (|alpha|, position) order. Any equal prefix sends the codeword to the exact slow
+    // path: beyond rank KMAX+1 the order cannot change this path's result, but an exact
+    // tie anywhere is flagged (BCHK_F_TIE) there, so every path reports the same flags.
     bool bad = (key[0] >> 6) == 0u                       // some |y| < 2^-27 (or zero)
                || (key[N - 1] >> 6) == 0x3FFFFFFu;       // some |y| >= 32, inf or NaN
 #pragma unroll
-    for (int r = 0; r <= KMAX && r < 63; ++r) bad |= ((key[r] ^ key[r + 1]) >> 6) == 0u;
-    auto alpha_at = [&](int pos) { return fabs((2.0 * yrow[pos]) / s2); };
+    for (int r = 0; r < N - 1; ++r) bad |= ((key[r] ^ key[r + 1]) >> 6) == 0u;
+    {   // materialise the flag here, so the sorted keys past the prefix die now
+        uint32_t b = bad ? 1u : 0u;
+        asm volatile("" : "+v"(b));
+        bad = b != 0u;
+    }
 
+    // ---- the sorted prefix calcRightSide can touch: positions packed 5 per word, their
+    // alphas computed once (IEEE f64 division, as the reference) from one batch of loads
+    constexpr int NPF = KMAX + 1;
+    constexpr int NPW = (NPF + 4) / 5;
+    uint32_t ppk[NPW];
+#pragma unroll
+    for (int w = 0; w < NPW; ++w) ppk[w] = 0;
+#pragma unroll
+    for (int r = 0; r < NPF; ++r) ppk[r / 5] |= (key[r] & 63u) << (6 * (r % 5));
+    auto ppos = [&](int r) { return (int)((ppk[r / 5] >> (6 * (r % 5))) & 63u); };
+    const int o0 = (int)(key[0] & 63u);
+    double apf[NPF];
+    {
+        double yv[NPF];
+#pragma unroll
+        for (int r = 0; r < NPF; ++r) yv[r] = yrow[ppos(r)];
+#pragma unroll
+        for (int r = 0; r < NPF; ++r) apf[r] = fabs((2.0 * yv[r]) / s2);
+    }
     // ---- syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
     uint32_t S0[W];
 #pragma unroll
@@ -159,20 +216,37 @@ kaneko_fast_kernel(SearchParams p) {
     }
 
     BCHK_STAMP(2)
-    // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`.
+#if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 3
+    if (p.l0 && live) p.l0[cw] = (double)(apf[0] + apf[NPF - 1] + (double)(S0[0] ^ ppk[0] ^ (uint32_t)bad));
+    return;
+#endif
+    // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`
+    // (at most t + 1 positions: the error pattern, plus the flipped bit at i = 1).
     auto accept = [&](uint64_t diff, double &l, bool &ret) {
+        constexpr int LMAX = TMAX + 1;
         const int m = __popcll(diff);
         const int border = (2 * t + 1) - m;  // m0 == m on both fast-path exits
+        double g[LMAX];
+        uint64_t v = diff;
+#pragma unroll
+        for (int j = 0; j < LMAX; ++j) {  // independent loads, issued together
+            g[j] = yrow[v ? (int)__builtin_ctzll(v) : 0];
+            v &= v - 1;
+        }
         l = 0.0;
-        for (uint64_t v = diff; v; v &= v - 1) l += alpha_at(__builtin_ctzll(v));
+        v = diff;
+#pragma unroll
+        for (int j = 0; j < LMAX; ++j) {
+            if (v) l += fabs((2.0 * g[j]) / s2);
+            v &= v - 1;
+        }
         double rs = 0.0;
         int taken = 0;
 #pragma unroll
-        for (int r = 0; r <= KMAX; ++r) {
-            const int o = (int)(key[r] & 63u);
-            const bool ag = !((diff >> o) & 1ull);
+        for (int r = 0; r < NPF; ++r) {
+            const bool ag = !((diff >> ppos(r)) & 1ull);
             if (ag && taken < border) {
-                rs += alpha_at(o);
+                rs += apf[r];
                 ++taken;
             }
         }
@@ -192,10 +266,13 @@ kaneko_fast_kernel(SearchParams p) {
         if (ret) { state = 1; best = E.w[0]; l0 = l; }
     }
     BCHK_STAMP(3)
+#if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 4
+    if (p.l0 && live) p.l0[cw] = (double)(l0 + (double)(state ^ (uint32_t)best));
+    return;
+#endif
     // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371)
     const bool need1 = live && !bad && !ok0;
     if (ballot(need1)) {
-        const int o0 = (int)(key[0] & 63u);
         uint32_t S1[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) S1[w] = S0[w] ^ col[o0 * W + w];
@@ -267,13 +344,18 @@ kaneko_fast_kernel(SearchParams p) {
 
 template <int M, int TMAX>
 static hipError_t launch_fast_impl(const SearchParams &p, size_t lds, hipStream_t s) {
-    const int blocks = (int)((p.count + 255u) / 256u);
-    hipLaunchKernelGGL((kaneko_fast_kernel<M, TMAX>), dim3(blocks), dim3(kWaveSize * kWavesPerBlock),
+    const uint32_t chunks = (p.count + 63u) / 64u;
+    const int blocks = (int)((chunks + kFastWaves - 1) / kFastWaves);
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void *)&kaneko_fast_kernel<M, TMAX>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((kaneko_fast_kernel<M, TMAX>), dim3(blocks), dim3(kWaveSize * kFastWaves),
                        lds, s, p);
     return hipGetLastError();
 }
 
 size_t fast_wave_bytes() { return (size_t)64 * kRowD * 8; }
+int fast_block_waves() { return kFastWaves; }
 
 // Fast-path instantiations (n <= 63, small t): (m, TMAX) as in select_kernels.
 bool select_fast(int m, int t, FastFn *out) {

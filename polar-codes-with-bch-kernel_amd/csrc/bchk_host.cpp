@@ -123,7 +123,7 @@ std::vector<uint8_t> make_tables(const Field &f, int t, TableDesc *td) {
     td->off_col = (uint32_t)off;
     off = align16(off + 4 * size_t(n) * W);
     td->off_chien = (uint32_t)off;
-    if (m <= 6) off = align16(off + 8 * size_t(t + 1) * (size_t(1) << m) * EW);
+    if (m <= 6) off = align16(off + 8 * size_t(t + 1) * 2 * size_t(m) * 8);
     td->bytes = (uint32_t)off;
     td->W = W;
     td->EW = EW;
@@ -140,16 +140,20 @@ std::vector<uint8_t> make_tables(const Field &f, int t, TableDesc *td) {
             col[p * W + j / 4] |= s << (8 * (j % 4));
         }
     if (m <= 6) {
+        // [j][half][b][8]: half 0 holds lo * alpha^(jk), half 1 holds (8 hi) * alpha^(jk)
         uint64_t *ch = reinterpret_cast<uint64_t *>(blob.data() + td->off_chien);
         for (int j = 0; j <= t; ++j)
-            for (unsigned v = 0; v < (1u << m); ++v) {
-                uint64_t *row = ch + (size_t((j << m) + v)) * EW;
-                for (int k = 0; k < n; ++k) {
-                    const unsigned val = f.mul(v, f.alog[(size_t(j) * k) % n]);
-                    for (int b = 0; b < m; ++b)
-                        if ((val >> b) & 1u) row[b] |= 1ull << k;
+            for (int half = 0; half < 2; ++half)
+                for (unsigned x = 0; x < 8; ++x) {
+                    const unsigned v = half ? (x << 3) : x;
+                    if (v >= (1u << m)) continue;
+                    for (int k = 0; k < n; ++k) {
+                        const unsigned val = f.mul(v, f.alog[(size_t(j) * k) % n]);
+                        for (int b = 0; b < m; ++b)
+                            if ((val >> b) & 1u)
+                                ch[((size_t(j) * 2 + half) * m + b) * 8 + x] |= 1ull << k;
+                    }
                 }
-            }
     }
     return blob;
 }
@@ -334,7 +338,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     const size_t tb = (c->td.bytes + 15) & ~size_t(15);
     c->lds = tb + kWavesPerBlock * c->ks.wave_bytes;
     c->lds_alg = tb;
-    if (select_fast(m, t, &c->fast)) c->lds_fast = tb + kWavesPerBlock * fast_wave_bytes();
+    if (select_fast(m, t, &c->fast)) c->lds_fast = tb + fast_block_waves() * fast_wave_bytes();
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);
     c->lds_coop = tb + c->ks.coop_bytes;

@@ -71,14 +71,22 @@ __device__ void prep_codeword(const SearchParams &p, const uint32_t *col, double
         P.av[s] = valid ? fabs(al) : 0.0;
         P.yH.w[s] = ballot(valid && !(al <= 0.0));
     }
-    // exact rank by (|alpha|, position): the stable order of std::sort's keys (:343)
+    // exact rank by (|alpha|, position): the stable order of std::sort's keys (:343).
+    // |alpha| by position goes to LDS first; every lane then streams all N values with
+    // broadcast reads (uniform address, no bank conflict) and counts those ranked before it.
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const int pos = lane + 64 * s;
+        if (pos < N) ap[pos] = P.av[s];
+    }
+    wave_sync();
     int rk[NW];
     bool tie = false;
 #pragma unroll
     for (int s = 0; s < NW; ++s) rk[s] = 0;
-#pragma unroll
+#pragma unroll 8
     for (int q = 0; q < N; ++q) {
-        const double aq = rdlf(P.av[q >> 6], q & 63);
+        const double aq = ap[q];
 #pragma unroll
         for (int s = 0; s < NW; ++s) {
             const int pos = lane + 64 * s;
@@ -94,7 +102,6 @@ __device__ void prep_codeword(const SearchParams &p, const uint32_t *col, double
         const int pos = lane + 64 * s;
         if (pos < N) {
             as[rk[s]] = P.av[s];
-            ap[pos] = P.av[s];
             ordl[rk[s]] = (uint8_t)pos;
         }
     }
@@ -425,8 +432,9 @@ kaneko_coop_kernel(SearchParams p) {
     uint64_t *diff_l = okm_l + kCoopWaves;                                      // [waves][64][NW]
     double *l_l = reinterpret_cast<double *>(diff_l + kCoopWaves * 64 * NW);    // [waves][64]
     uint32_t *m_l = reinterpret_cast<uint32_t *>(l_l + kCoopWaves * 64);        // [waves][64]
-    uint64_t *ctl = reinterpret_cast<uint64_t *>(m_l + kCoopWaves * 64);        // bound, done, item
-    uint8_t *wbase = reinterpret_cast<uint8_t *>(ctl + 4) + wid * Smem<M, TMAX>::WAVE_BYTES;
+    uint64_t *ctl = reinterpret_cast<uint64_t *>(m_l + kCoopWaves * 64);  // bound, done, item, l0
+    uint64_t *cand_l = ctl + 4;                                           // [waves]
+    uint8_t *wbase = reinterpret_cast<uint8_t *>(cand_l + kCoopWaves) + wid * Smem<M, TMAX>::WAVE_BYTES;
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
@@ -452,27 +460,46 @@ kaneko_coop_kernel(SearchParams p) {
 #endif
         SearchState<NW> S;
         init_state<M>(S, p.variant);
-        if (threadIdx.x == 0) { ctl[0] = S.bound; ctl[1] = 0; }
+        if (threadIdx.x == 0) {
+            ctl[0] = S.bound;
+            ctl[1] = 0;
+            ctl[3] = (uint64_t)__double_as_longlong(S.l0);
+        }
         for (uint64_t rbase = 0;; rbase += 64 * kCoopWaves) {
             __syncthreads();
             const uint64_t bound = ctl[0];
             if (ctl[1]) break;
+            const double l0r = __longlong_as_double((long long)ctl[3]);  // l0 at round start
             const uint64_t base = rbase + 64 * (uint64_t)wid;
-            uint64_t okm = 0;
+            uint64_t okm = 0, cand = 0;
             if (base < bound && !(p.max_decodes && base >= p.max_decodes)) {
                 Mask<NW> diff;
                 int m;
                 double l;
                 const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, diff, m, l);
-                okm = ballot(ok && base + (uint64_t)lane < bound);
-                if (ok) {
+                const bool live = ok && base + (uint64_t)lane < bound;
+                okm = ballot(live);
+                // candidates: the strict running minima of l over this wave's successes,
+                // below the round-start l0. The round's improvements are the running minima
+                // over all its successes in pattern order, so they are a subset of these.
+                const uint64_t cm = ballot(live && l < l0r);
+                double run = l0r;
+                for (uint64_t mm = cm; mm; mm &= mm - 1) {
+                    const int L = (int)__builtin_ctzll(mm);
+                    const double lv = rdlf(l, L);
+                    if (lv < run) {
+                        cand |= 1ull << L;
+                        run = lv;
+                    }
+                }
+                if ((cand >> lane) & 1ull) {
 #pragma unroll
                     for (int s = 0; s < NW; ++s) diff_l[(wid * 64 + lane) * NW + s] = diff.w[s];
                     m_l[wid * 64 + lane] = (uint32_t)m;
                 }
                 l_l[wid * 64 + lane] = l;
             }
-            if (lane == 0) okm_l[wid] = okm;
+            if (lane == 0) { okm_l[wid] = okm; cand_l[wid] = cand; }
 #ifdef BCHK_DIAG
             const unsigned long long t_dec = __builtin_amdgcn_s_memtime();
 #endif
@@ -485,46 +512,31 @@ kaneko_coop_kernel(SearchParams p) {
             const uint64_t impr0 = S.impr;
 #endif
             if (wid == 0) {
-                // All 16 waves' success masks and calcL values in one batch of LDS reads;
-                // the next improvement (l < l0, in pattern order) is found with 16 ballots
-                // from registers, and accept_success runs once per improvement (rare).
-                uint64_t okw[kCoopWaves];
-                double lw[kCoopWaves];
-#pragma unroll
-                for (int w = 0; w < kCoopWaves; ++w) {
-                    okw[w] = okm_l[w];
-                    lw[w] = l_l[w * 64 + lane];
-                }
-                if (rbase == 0 && !(okw[0] & 1ull)) S.firstOK = false;  // :371
+                // Visit the round's candidates in pattern order; accept_success runs for
+                // those that still improve on the current l0 (rare).
+                if (rbase == 0 && !(okm_l[0] & 1ull)) S.firstOK = false;  // :371
                 // patterns this round may run to: the loop bound, or the safety cap rounded
                 // up to its 64-pattern chunk (as the single-wave kernel applies it)
                 const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63) & ~63ull) : ~0ull;
-                uint64_t stop = S.bound < capc ? S.bound : capc;
-                int from = 0;  // linear index (64 w + lane) to search from
-                for (;;) {
-                    int fw = -1, fl = 0;
+                // lane w < 16 holds wave w's candidate mask: one LDS read, one ballot
+                const uint64_t cv = lane < kCoopWaves ? cand_l[lane] : 0ull;
+                for (uint64_t wm = ballot(cv != 0ull); wm && !S.done; wm &= wm - 1) {
+                    const int w = (int)__builtin_ctzll(wm);
+                    uint64_t im = rdl64(cv, w);
+                    while (im && !S.done) {
+                        const int fl = (int)__builtin_ctzll(im);
+                        im &= im - 1;
+                        const uint64_t ii = rbase + 64 * (uint64_t)w + (uint64_t)fl;
+                        const uint64_t stop = S.bound < capc ? S.bound : capc;
+                        if (ii >= stop) { im = 0; break; }
+                        const double lL = l_l[w * 64 + fl];
+                        if (!(lL < S.l0)) continue;
+                        const int mL = (int)m_l[w * 64 + fl];
+                        Mask<NW> d;
 #pragma unroll
-                    for (int w = kCoopWaves - 1; w >= 0; --w) {
-                        uint64_t im = ballot(((okw[w] >> lane) & 1ull) && lw[w] < S.l0);
-                        const int lo = from - 64 * w;  // lanes below `from` are done
-                        im = lo <= 0 ? im : (lo >= 64 ? 0ull : (im & ~((1ull << lo) - 1ull)));
-                        if (im) { fw = w; fl = (int)__builtin_ctzll(im); }
+                        for (int s2 = 0; s2 < NW; ++s2) d.w[s2] = diff_l[(w * 64 + fl) * NW + s2];
+                        accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
                     }
-                    if (fw < 0) break;
-                    const uint64_t ii = rbase + 64 * (uint64_t)fw + (uint64_t)fl;
-                    if (ii >= stop) break;
-                    double lsel = 0.0;
-#pragma unroll
-                    for (int w = 0; w < kCoopWaves; ++w) lsel = (w == fw) ? lw[w] : lsel;
-                    const double lL = rdlf(lsel, fl);
-                    const int mL = (int)m_l[fw * 64 + fl];
-                    Mask<NW> d;
-#pragma unroll
-                    for (int s = 0; s < NW; ++s) d.w[s] = diff_l[(fw * 64 + fl) * NW + s];
-                    accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
-                    if (S.done) break;
-                    stop = S.bound < capc ? S.bound : capc;
-                    from = 64 * fw + fl + 1;
                 }
                 // the loop ends in this round when it reaches the bound, or is cut at the
                 // cap; whichever chunk comes first (the bound wins a tie), as the
@@ -540,7 +552,11 @@ kaneko_coop_kernel(SearchParams p) {
                         S.done = true;
                     }
                 }
-                if (lane == 0) { ctl[0] = S.bound; ctl[1] = S.done ? 1u : 0u; }
+                if (lane == 0) {
+                    ctl[0] = S.bound;
+                    ctl[1] = S.done ? 1u : 0u;
+                    ctl[3] = (uint64_t)__double_as_longlong(S.l0);
+                }
             }
 #ifdef BCHK_DIAG
             t_prev = __builtin_amdgcn_s_memtime();
@@ -656,7 +672,7 @@ template <int M, int TMAX>
 static KernelSet make_set() {
     constexpr int NW = Geo<M>::NW;
     const size_t coop = (size_t)kCoopWaves * 8 + (size_t)kCoopWaves * 64 * NW * 8 +
-                        (size_t)kCoopWaves * 64 * 12 + 32 +
+                        (size_t)kCoopWaves * 64 * 12 + 32 + (size_t)kCoopWaves * 8 +
                         (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES;
     return KernelSet{&launch_search_impl<M, TMAX>, &launch_coop_impl<M, TMAX>, &coop_fn<M, TMAX>, coop,
                      &launch_alg_impl<M, TMAX>, &search_fn<M, TMAX>, TMAX,

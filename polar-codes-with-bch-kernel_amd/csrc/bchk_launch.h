@@ -22,6 +22,7 @@ typedef hipError_t (*FastFn)(const SearchParams &, size_t, hipStream_t);
 // Lane-per-codeword fast path (bchk_fast.hip); false when (m, t) has none (n > 63, large t).
 bool select_fast(int m, int t, FastFn *out);
 size_t fast_wave_bytes();
+int fast_block_waves();  // waves per block of the fast kernel
 
 // Picks the (m, TMAX) instantiation for runtime t (smallest TMAX >= t).
 bool select_kernels(int m, int t, KernelSet *out);

@@ -17,6 +17,7 @@ for CNT in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 cd $ROOT
+[ "${PMC_NO_SWEEP:-0}" = 1 ] && exit 0
 for CL in 0 2 4 8 16; do
   BCHK_CHUNK_LIMIT=$CL timeout -k 10 300 python bench.py --steps 5 --warmup 1 --cpu-seconds 0 > $OUT/${TAG}_cl$CL.json 2>/dev/null
   rc=$?; echo "chunk_limit $CL rc=$rc"; [ $rc -eq 0 ] || exit $rc
