@@ -241,6 +241,37 @@ __device__ __forceinline__ uint32_t sp_mul(uint32_t a, uint32_t b) {
     }
     return r;
 }
+// Reduction of a raw product, or of the XOR of several raw products (the slot parities
+// add, the bits between slots are junk that never reaches a slot): one fold per product
+// sum instead of one per product ("lazy" reduction).
+template <int M>
+__device__ __forceinline__ uint32_t sp_red(uint32_t r) {
+    static_assert(M <= 6, "spread GF arithmetic needs m <= 6");
+    if constexpr (Spread<M>::FOLDS == 1) {
+        // x^(m+k) = x^k q(x): the high slots shifted by 3b for every term x^b of q; junk
+        // bits move by multiples of 3 and stay between slots, so one final mask suffices
+        const uint32_t h = r >> (3 * M);
+        uint32_t f = r;
+#pragma unroll
+        for (int b = 0; b < M; ++b)
+            if ((Spread<M>::Q >> b) & 1u) f ^= h << (3 * b);
+        return f & Spread<M>::ELEM;
+    } else {
+        r &= Spread<M>::PROD;
+#pragma unroll
+        for (int f = 0; f < Spread<M>::FOLDS; ++f) {
+            const uint32_t h = r >> (3 * M);
+            r &= Spread<M>::ELEM;
+#pragma unroll
+            for (int b = 0; b < M; ++b)
+                if ((Spread<M>::Q >> b) & 1u) r ^= h << (3 * b);
+        }
+        return r;
+    }
+}
+// raw carry-less product of two reduced spread elements (no reduction)
+__device__ __forceinline__ uint32_t sp_raw(uint32_t a, uint32_t b) { return __umul24(a, b); }
+
 __device__ __forceinline__ uint32_t sp_from(uint32_t v) {  // 6-bit element -> spread
     v &= 0x3Fu;
     v = (v | (v << 8)) & 0x0000F00Fu;
@@ -266,7 +297,8 @@ __device__ __forceinline__ bool alg_core_valu(const uint64_t *__restrict__ chien
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) S[2 * j] = sp_from((Sw[j >> 2] >> (8 * (j & 3))) & 0xFFu);
 #pragma unroll
-    for (int e = 2; e <= 2 * TMAX - 1; e += 2) S[e - 1] = sp_mul<M>(S[e / 2 - 1], S[e / 2 - 1]);
+    for (int e = 2; e <= 2 * TMAX - 1; e += 2)
+        S[e - 1] = sp_red<M>(sp_raw(S[e / 2 - 1], S[e / 2 - 1]));
     uint32_t C[TMAX + 1], B[TMAX + 1];
 #pragma unroll
     for (int i = 0; i <= TMAX; ++i) { C[i] = i ? 0u : 1u; B[i] = i ? 0u : 1u; }
@@ -276,17 +308,18 @@ __device__ __forceinline__ bool alg_core_valu(const uint64_t *__restrict__ chien
     for (int k = 0; k < TMAX; ++k) {
         if (k < t) {
             const int r = 2 * k;
-            uint32_t d = 0;
+            uint32_t dr = 0;  // discrepancy: XOR of raw products, reduced once
 #pragma unroll
             for (int i = 0; i <= (2 * k - 1 > 0 ? (2 * k - 1 < TMAX ? 2 * k - 1 : TMAX) : 0); ++i)
-                d ^= sp_mul<M>(C[i], S[r - i]);
+                dr ^= sp_raw(C[i], S[r - i]);
+            const uint32_t d = sp_red<M>(dr);
             const bool chg = (d != 0u) && (2 * L <= r);
             uint32_t Cn[TMAX + 1];
 #pragma unroll
             for (int i = 0; i <= TMAX; ++i) {
                 if (i > 2 * k + 1) { Cn[i] = 0u; continue; }
-                const uint32_t g = sp_mul<M>(gam, C[i]);
-                Cn[i] = i ? (g ^ sp_mul<M>(d, B[i - 1])) : g;
+                const uint32_t g = sp_raw(gam, C[i]);
+                Cn[i] = sp_red<M>(i ? (g ^ sp_raw(d, B[i - 1])) : g);
             }
 #pragma unroll
             for (int i = TMAX; i >= 0; --i) {

@@ -411,15 +411,54 @@ kaneko_search_kernel(SearchParams p) {
 }
 
 // ---------------------------------------- cooperative search of heavy codewords
-// One workgroup of kCoopWaves waves per codeword: every round, wave w decodes patterns
-// [base + 64 w, base + 64 w + 64); wave 0 then applies the reference's sequential
-// acceptance to all successes of the round in pattern order (:361-405) and publishes the
-// new loop bound. Results are identical to the single-wave search.
+// One workgroup per codeword: kCoopWaves - 1 decoder waves and one acceptor wave.
+// Decoders take 64-pattern chunks from an LDS counter (the oldest waves, which the SIMD
+// favours, simply take more) and decode them speculatively ahead of the acceptance; each
+// finished chunk lands in a ring of kCoopSlots slots (success mask, candidates). The
+// acceptor walks the chunks strictly in pattern order, applies the reference's sequential
+// acceptance (:361-405) to the candidates, and publishes the loop bound and l0 that the
+// decoders read to stop early and filter candidates. No workgroup barrier per chunk.
+// Results are identical to the single-wave search.
+constexpr int kCoopSlots = 16;
+constexpr uint32_t kSpinLimit = 1u << 24;  // ~1 s of polling: a guard against logic errors
+
+template <int NW>
+struct CoopSlot {  // one decoded chunk
+    uint64_t okm, cand;
+    uint64_t diff[64 * NW];
+    double l[64];
+    uint32_t m[64];
+};
+
+struct CoopCtl {
+    uint32_t next;      // next chunk to hand out
+    uint32_t consumed;  // chunks the acceptor has finished
+    uint32_t done;      // the codeword's search has ended
+    uint32_t item;      // heavy-queue item of this workgroup
+    uint64_t bound;     // current loop bound (monotone non-increasing)
+    double l0;          // current l0 (monotone non-increasing)
+    uint32_t ready[kCoopSlots];  // chunk index + 1 once the slot holds that chunk
+};
+
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t *a, uint32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint64_t lds_ld64(const uint64_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st64(uint64_t *a, uint64_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int M, int TMAX>
 __global__ void __launch_bounds__(kWaveSize * kCoopWaves)
 kaneko_coop_kernel(SearchParams p) {
-    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    constexpr int NW = Geo<M>::NW;
     constexpr int NP = Smem<M, TMAX>::NP;
+    constexpr int kAcceptor = 0;  // the oldest wave: the SIMD arbiter favours it
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
     const uint8_t *ex = smem + p.td.off_exp;
@@ -428,61 +467,76 @@ kaneko_coop_kernel(SearchParams p) {
     const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint8_t *shared0 = smem + ((p.td.bytes + 15) & ~15u);
-    uint64_t *okm_l = reinterpret_cast<uint64_t *>(shared0);                    // [waves]
-    uint64_t *diff_l = okm_l + kCoopWaves;                                      // [waves][64][NW]
-    double *l_l = reinterpret_cast<double *>(diff_l + kCoopWaves * 64 * NW);    // [waves][64]
-    uint32_t *m_l = reinterpret_cast<uint32_t *>(l_l + kCoopWaves * 64);        // [waves][64]
-    uint64_t *ctl = reinterpret_cast<uint64_t *>(m_l + kCoopWaves * 64);  // bound, done, item, l0
-    uint64_t *cand_l = ctl + 4;                                           // [waves]
-    uint8_t *wbase = reinterpret_cast<uint8_t *>(cand_l + kCoopWaves) + wid * Smem<M, TMAX>::WAVE_BYTES;
+    CoopSlot<NW> *ring = reinterpret_cast<CoopSlot<NW> *>(shared0);
+    CoopCtl *ctl = reinterpret_cast<CoopCtl *>(ring + kCoopSlots);
+    uint8_t *wbase = reinterpret_cast<uint8_t *>(ctl + 1) + wid * Smem<M, TMAX>::WAVE_BYTES;
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
     const uint32_t total = *p.heavy_tail;
+    const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63) & ~63ull) : ~0ull;
     for (;;) {
         __syncthreads();
-        if (threadIdx.x == 0) ctl[2] = atomicAdd(p.heavy_head, 1u);
+        if (threadIdx.x == 0) {
+            ctl->item = atomicAdd(p.heavy_head, 1u);
+            ctl->next = 0;
+            ctl->consumed = 0;
+            ctl->done = 0;
+        }
+        if (threadIdx.x < kCoopSlots) ctl->ready[threadIdx.x] = 0;
         __syncthreads();
-        const uint32_t item = (uint32_t)ctl[2];
+        const uint32_t item = ctl->item;
         if (item >= total) return;
         const uint32_t cw = p.heavy_queue[item];
 #ifdef BCHK_DIAG
-        // stamps (wave 0): [0] prep, [1] own decodes, [2] wait for the other waves,
-        // [3] ordered acceptance, [4] rounds, [5] improvements, [6] total
+        // stamps (acceptor): [0] prep, [1] waiting for chunks, [2] acceptance, [3] chunks
+        // decoded (all waves), [4] chunks accepted, [5] improvements, [6] total
         unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
         Prep<M, TMAX> P;  // every wave builds the same prep (its own LDS slice)
         prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+        SearchState<NW> S;
+        init_state<M>(S, p.variant);
+        if (threadIdx.x == 0) {
+            ctl->bound = S.bound;
+            ctl->l0 = S.l0;
+        }
+        __syncthreads();
 #ifdef BCHK_DIAG
         unsigned long long t_prev = __builtin_amdgcn_s_memtime();
         dg[0] = t_prev - t_start;
 #endif
-        SearchState<NW> S;
-        init_state<M>(S, p.variant);
-        if (threadIdx.x == 0) {
-            ctl[0] = S.bound;
-            ctl[1] = 0;
-            ctl[3] = (uint64_t)__double_as_longlong(S.l0);
-        }
-        for (uint64_t rbase = 0;; rbase += 64 * kCoopWaves) {
-            __syncthreads();
-            const uint64_t bound = ctl[0];
-            if (ctl[1]) break;
-            const double l0r = __longlong_as_double((long long)ctl[3]);  // l0 at round start
-            const uint64_t base = rbase + 64 * (uint64_t)wid;
-            uint64_t okm = 0, cand = 0;
-            if (base < bound && !(p.max_decodes && base >= p.max_decodes)) {
+        if (wid != kAcceptor) {
+            // ------------------------------------------------------------ decoder
+            for (;;) {
+                uint32_t c = 0;
+                if (lane == 0) c = atomicAdd(&ctl->next, 1u);
+                c = (uint32_t)__shfl((int)c, 0, 64);
+                const uint64_t base = 64ull * c;
+                uint64_t bound = lds_ld64(&ctl->bound);
+                if (base >= bound || base >= capc || lds_ld(&ctl->done)) break;
+                // the slot is free once the acceptor has finished chunk c - kCoopSlots
+                bool stop = false;
+                for (uint32_t spins = 0; c >= lds_ld(&ctl->consumed) + kCoopSlots; ++spins) {
+                    if (lds_ld(&ctl->done) || spins > kSpinLimit) { stop = true; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (stop) break;
+                bound = lds_ld64(&ctl->bound);
+                const double l0r = __longlong_as_double((long long)lds_ld64(
+                    reinterpret_cast<const uint64_t *>(&ctl->l0)));
                 Mask<NW> diff;
                 int m;
                 double l;
                 const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, diff, m, l);
                 const bool live = ok && base + (uint64_t)lane < bound;
-                okm = ballot(live);
-                // candidates: the strict running minima of l over this wave's successes,
-                // below the round-start l0. The round's improvements are the running minima
-                // over all its successes in pattern order, so they are a subset of these.
+                const uint64_t okm = ballot(ok);
+                // candidates: the strict running minima of l over this chunk's successes,
+                // below l0 as last published. The improvements are the running minima over
+                // all successes in pattern order, so they are a subset of these.
                 const uint64_t cm = ballot(live && l < l0r);
+                uint64_t cand = 0;
                 double run = l0r;
                 for (uint64_t mm = cm; mm; mm &= mm - 1) {
                     const int L = (int)__builtin_ctzll(mm);
@@ -492,91 +546,119 @@ kaneko_coop_kernel(SearchParams p) {
                         run = lv;
                     }
                 }
+                CoopSlot<NW> &sl = ring[c % kCoopSlots];
                 if ((cand >> lane) & 1ull) {
 #pragma unroll
-                    for (int s = 0; s < NW; ++s) diff_l[(wid * 64 + lane) * NW + s] = diff.w[s];
-                    m_l[wid * 64 + lane] = (uint32_t)m;
-                }
-                l_l[wid * 64 + lane] = l;
-            }
-            if (lane == 0) { okm_l[wid] = okm; cand_l[wid] = cand; }
-#ifdef BCHK_DIAG
-            const unsigned long long t_dec = __builtin_amdgcn_s_memtime();
-#endif
-            __syncthreads();
-#ifdef BCHK_DIAG
-            const unsigned long long t_bar = __builtin_amdgcn_s_memtime();
-            dg[1] += t_dec - t_prev;
-            dg[2] += t_bar - t_dec;
-            dg[4] += 1;
-            const uint64_t impr0 = S.impr;
-#endif
-            if (wid == 0) {
-                // Visit the round's candidates in pattern order; accept_success runs for
-                // those that still improve on the current l0 (rare).
-                if (rbase == 0 && !(okm_l[0] & 1ull)) S.firstOK = false;  // :371
-                // patterns this round may run to: the loop bound, or the safety cap rounded
-                // up to its 64-pattern chunk (as the single-wave kernel applies it)
-                const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63) & ~63ull) : ~0ull;
-                // lane w < 16 holds wave w's candidate mask: one LDS read, one ballot
-                const uint64_t cv = lane < kCoopWaves ? cand_l[lane] : 0ull;
-                for (uint64_t wm = ballot(cv != 0ull); wm && !S.done; wm &= wm - 1) {
-                    const int w = (int)__builtin_ctzll(wm);
-                    uint64_t im = rdl64(cv, w);
-                    while (im && !S.done) {
-                        const int fl = (int)__builtin_ctzll(im);
-                        im &= im - 1;
-                        const uint64_t ii = rbase + 64 * (uint64_t)w + (uint64_t)fl;
-                        const uint64_t stop = S.bound < capc ? S.bound : capc;
-                        if (ii >= stop) { im = 0; break; }
-                        const double lL = l_l[w * 64 + fl];
-                        if (!(lL < S.l0)) continue;
-                        const int mL = (int)m_l[w * 64 + fl];
-                        Mask<NW> d;
-#pragma unroll
-                        for (int s2 = 0; s2 < NW; ++s2) d.w[s2] = diff_l[(w * 64 + fl) * NW + s2];
-                        accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
-                    }
-                }
-                // the loop ends in this round when it reaches the bound, or is cut at the
-                // cap; whichever chunk comes first (the bound wins a tie), as the
-                // single-wave kernel decides at its chunk starts
-                if (!S.done) {
-                    const uint64_t rend = rbase + 64 * (uint64_t)kCoopWaves;
-                    const uint64_t nb = (S.bound + 63) & ~63ull;
-                    if (nb <= capc) {
-                        if (S.bound <= rend) { S.i_end = S.bound; S.done = true; }
-                    } else if (capc <= rend) {
-                        S.i_end = capc;
-                        S.truncated = true;
-                        S.done = true;
-                    }
+                    for (int s2 = 0; s2 < NW; ++s2) sl.diff[lane * NW + s2] = diff.w[s2];
+                    sl.m[lane] = (uint32_t)m;
+                    sl.l[lane] = l;
                 }
                 if (lane == 0) {
-                    ctl[0] = S.bound;
-                    ctl[1] = S.done ? 1u : 0u;
-                    ctl[3] = (uint64_t)__double_as_longlong(S.l0);
+                    sl.okm = okm;
+                    sl.cand = cand;
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) lds_st(&ctl->ready[c % kCoopSlots], c + 1u);
+#ifdef BCHK_DIAG
+                dg[3] += 1;
+#endif
             }
+        } else {
+            // ------------------------------------------------------------ acceptor
+            __builtin_amdgcn_s_setprio(3);
+            uint32_t spins = 0;
+            for (uint32_t c = 0; !S.done;) {
+                // the loop ends at the bound, or is cut at the cap (chunk-granular, the
+                // bound winning a tie) exactly as the single-wave kernel decides
+                {
+                    const uint64_t nb = (S.bound + 63) & ~63ull;  // first chunk past the bound
+                    if (64ull * c >= nb || 64ull * c >= capc) {
+                        if (nb <= capc) {
+                            S.i_end = S.bound;
+                        } else {
+                            S.i_end = capc;
+                            S.truncated = true;
+                        }
+                        break;
+                    }
+                }
 #ifdef BCHK_DIAG
-            t_prev = __builtin_amdgcn_s_memtime();
-            dg[3] += t_prev - t_bar;
-            dg[5] += S.impr - impr0;
+                const unsigned long long t_w = __builtin_amdgcn_s_memtime();
 #endif
+                // lane j looks at chunk c + j: the run of consecutive finished chunks is
+                // taken in one batch (one LDS round trip for flags, one for the masks)
+                const uint32_t cj = c + (uint32_t)lane;
+                const bool rdy = lane < kCoopSlots && lds_ld(&ctl->ready[cj % kCoopSlots]) == cj + 1u;
+                const uint64_t rm = ballot(rdy);
+                const int run = (int)__builtin_ctzll(~rm);  // chunks c .. c + run - 1 ready
+                if (run == 0) {
+                    if (++spins > kSpinLimit) {  // never expected: fail the codeword, no hang
+                        S.i_end = 64ull * c;
+                        S.truncated = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                spins = 0;
+#ifdef BCHK_DIAG
+                const unsigned long long t_a = __builtin_amdgcn_s_memtime();
+                dg[1] += t_a - t_w;
+                const uint64_t impr0 = S.impr;
+#endif
+                const uint64_t candj = lane < run ? ring[cj % kCoopSlots].cand : 0ull;
+                if (c == 0 && !(ring[0].okm & 1ull)) S.firstOK = false;  // :371
+                uint32_t cdone = c + (uint32_t)run;
+                for (uint64_t jm = ballot(candj != 0ull); jm; jm &= jm - 1) {
+                    const int j = (int)__builtin_ctzll(jm);
+                    const uint32_t cc = c + (uint32_t)j;
+                    const uint64_t base = 64ull * cc;
+                    if (base >= S.bound || base >= capc) { cdone = cc; break; }
+                    const CoopSlot<NW> &sl = ring[cc % kCoopSlots];
+                    for (uint64_t im = rdl64(candj, j); im; im &= im - 1) {
+                        const int L = (int)__builtin_ctzll(im);
+                        const uint64_t ii = base + (uint64_t)L;
+                        if (ii >= S.bound) break;
+                        const double lL = sl.l[L];
+                        if (!(lL < S.l0)) continue;
+                        Mask<NW> d;
+#pragma unroll
+                        for (int s2 = 0; s2 < NW; ++s2) d.w[s2] = sl.diff[L * NW + s2];
+                        accept_success<M, TMAX>(S, P, d, (int)sl.m[L], lL, ii, as, p, lane);
+                        if (S.done) break;
+                    }
+                    if (S.done) { cdone = cc + 1u; break; }
+                }
+                c = cdone;
+                if (lane == 0) {
+                    lds_st64(&ctl->bound, S.bound);
+                    lds_st64(reinterpret_cast<uint64_t *>(&ctl->l0),
+                             (uint64_t)__double_as_longlong(S.l0));
+                    lds_st(&ctl->consumed, c);
+                }
+#ifdef BCHK_DIAG
+                dg[2] += __builtin_amdgcn_s_memtime() - t_a;
+                dg[4] += (uint64_t)run;
+                dg[5] += S.impr - impr0;
+#endif
+            }
+            __builtin_amdgcn_s_setprio(0);
+            if (lane == 0) lds_st(&ctl->done, 1u);
+            write_outputs<M, TMAX>(S, P, p, cw, lane);
         }
-        if (wid == 0) write_outputs<M, TMAX>(S, P, p, cw, lane);
 #ifdef BCHK_DIAG
-        dg[6] = __builtin_amdgcn_s_memtime() - t_start;
-        dg[7] = cw;
-        if (p.diag && threadIdx.x == 0)
-            for (int q = 0; q < 8; ++q) p.diag[(size_t)item * 8 + q] = dg[q];
+        // chunk counts of every wave into the acceptor's record
+        if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long *>(&p.diag[(size_t)item * 8 + 3]), dg[3]);
+        if (wid == kAcceptor && lane == 0) {
+            dg[6] = __builtin_amdgcn_s_memtime() - t_start;
+            dg[7] = cw;
+            for (int q = 0; q < 8; ++q)
+                if (q != 3) p.diag[(size_t)item * 8 + q] = dg[q];
+        }
 #endif
-        (void)N;
     }
 }
 
-// ------------------------------------------------- batched algebraic decoder
-// Decoder::decode (src/Decoder.cpp:298-321), one word per lane.
 template <int M, int TMAX>
 __global__ void __launch_bounds__(256) alg_decode_kernel(AlgParams p) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
@@ -671,8 +753,7 @@ static const void *coop_fn() { return reinterpret_cast<const void *>(&kaneko_coo
 template <int M, int TMAX>
 static KernelSet make_set() {
     constexpr int NW = Geo<M>::NW;
-    const size_t coop = (size_t)kCoopWaves * 8 + (size_t)kCoopWaves * 64 * NW * 8 +
-                        (size_t)kCoopWaves * 64 * 12 + 32 + (size_t)kCoopWaves * 8 +
+    const size_t coop = sizeof(CoopSlot<NW>) * kCoopSlots + sizeof(CoopCtl) +
                         (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES;
     return KernelSet{&launch_search_impl<M, TMAX>, &launch_coop_impl<M, TMAX>, &coop_fn<M, TMAX>, coop,
                      &launch_alg_impl<M, TMAX>, &search_fn<M, TMAX>, TMAX,

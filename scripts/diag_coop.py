@@ -21,7 +21,7 @@ _, n_coop = d.path_counts()
 buf = np.zeros((n_coop, 8), np.uint64)
 assert L.bchk_diag_read(d.handle, buf.ctypes.data, n_coop) == 0
 dec = st["decodes"][buf[:, 7].astype(np.int64)]
-names = ["prep", "own_decode", "wait_others", "accept", "rounds", "improvements", "total"]
+names = ["prep", "wait_chunks", "accept", "chunks_decoded", "chunks_accepted", "improvements", "total"]
 out = {"n": int(n_coop), "sum": {k: int(buf[:, i].sum()) for i, k in enumerate(names)}}
 top = np.argsort(-buf[:, 6].astype(np.int64))[:8]
 out["top"] = [{**{k: int(buf[j, i]) for i, k in enumerate(names)}, "decodes": int(dec[j])} for j in top]
