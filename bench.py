@@ -168,7 +168,6 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        dec.profile(True)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
@@ -177,7 +176,14 @@ def main():
         elapsed = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-    ms3, calls = dec.profile_read()
+        # per-kernel durations: the same steps again with HIP events around every launch
+        # (outside the timed region, so event records do not perturb `value`)
+        dec.profile(True)
+        for _ in range(args.steps):
+            step()
+        dec.sync()
+        torch.cuda.synchronize()
+    ms3, launches = dec.profile_read()  # launches: sub-batch launches per stage
     dec.profile(False)
     n_exact, n_coop = dec.path_counts()
     elapsed = max_over_ranks(elapsed, world, dist, dev)
@@ -188,14 +194,18 @@ def main():
     # out. The fast kernel moves them for all B codewords; the exact and
     # cooperative kernels re-read/write them for the codewords handed to them.
     bytes_per_cw = 9 * n + 8
-    calls = max(1, calls)
+    launches = max(1, launches)
+    pipe = max(1, launches // args.steps)  # sub-batches per decode call (stream pipeline)
     tm = dec_tmax(args.t)
     fast_on = ms3[0] > 0 and n_exact < B
-    kern = [{"name": f"kaneko_fast_kernel<{args.m},{tm}>", "ms": ms3[0] / calls, "codewords": B},
-            {"name": f"kaneko_search_kernel<{args.m},{tm}>", "ms": ms3[1] / calls,
-             "codewords": int(n_exact) if fast_on else B},
-            {"name": f"kaneko_coop_kernel<{args.m},{tm}>", "ms": ms3[2] / calls,
-             "codewords": int(n_coop)}]
+    # per launch: average duration (HIP events on the launching stream) and the codewords
+    # one launch processes (the last call's hand-off counts, spread over its sub-batches)
+    kern = [{"name": f"kaneko_fast_kernel<{args.m},{tm}>", "ms": ms3[0] / launches,
+             "codewords": B / pipe},
+            {"name": f"kaneko_search_kernel<{args.m},{tm}>", "ms": ms3[1] / launches,
+             "codewords": (n_exact if fast_on else B) / pipe},
+            {"name": f"kaneko_coop_kernel<{args.m},{tm}>", "ms": ms3[2] / launches,
+             "codewords": n_coop / pipe}]
     for k in kern:
         k["GB_s"] = (bytes_per_cw * k["codewords"] / (k["ms"] / 1e3) / 1e9) if k["ms"] > 0 else 0.0
     dom = max(kern, key=lambda k: k["ms"])
@@ -235,7 +245,8 @@ def main():
             "kernels": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in kk.items()}
                         for kk in kern],
             "dominant_kernel": dom["name"],
-            "decode_ms": round(sum(k["ms"] for k in kern), 4),
+            "sub_batches_per_step": pipe,
+            "kernel_ms_per_step": round(pipe * sum(k["ms"] for k in kern), 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic},

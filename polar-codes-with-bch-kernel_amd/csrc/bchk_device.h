@@ -11,6 +11,7 @@ constexpr int kMaxM = 8;
 constexpr int kMaxT = 32;
 constexpr int kWaveSize = 64;
 constexpr int kWavesPerBlock = 4;
+constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
 
 // Per-code lookup tables, one device blob, copied into LDS by every workgroup.
 //   exp8 [2n]        alpha^i for i < 2n-1, exp8[2n-1] = 0 (log sums are clamped to
@@ -48,14 +49,26 @@ struct SearchParams {
     uint32_t *qtail;       // fast path: append unresolved codewords here (with queue_out)
     uint32_t *queue_out;
     // heavy codewords: the wave kernel hands a codeword still running after chunk_limit
-    // steps of 64 patterns to the cooperative kernel (heavy_queue[*heavy_tail++]);
-    // heavy_tail == null disables the hand-off.
+    // steps of 64 patterns to the cooperative kernel, which may run concurrently with it
+    // (heavy_tail == null disables the hand-off). Longest-first: codewords whose loop bound
+    // at the hand-off is >= heavy_big go to the front queue (slots 0, 1, ...), the others to
+    // the back queue (slots count-1, count-2, ...). A producer reserves a slot with its
+    // tail, then stores the codeword index; empty slots hold kEmptySlot, and consumers
+    // (who reserve with the heads) put it back, so the array stays clean between calls.
+    // exact_done counts the codewords the wave kernel has finished or handed off; once it
+    // reaches *exact_total (null: count) the tails are final.
     uint32_t *heavy_queue;
     uint32_t *heavy_tail;
+    uint32_t *heavy_tail2;
     uint32_t *heavy_head;
+    uint32_t *heavy_head2;
+    uint32_t *exact_done;
+    const uint32_t *exact_total;
+    uint64_t heavy_big;
     uint32_t chunk_limit;
     // diagnostic builds only (-DBCHK_DIAG): per heavy-queue item, 8 u64 timing counters
     unsigned long long *diag;
+    uint32_t *diag_count;
     int32_t t;
     int32_t J;             // < 0: shipped
     int32_t variant;       // BCHK_VARIANT_*

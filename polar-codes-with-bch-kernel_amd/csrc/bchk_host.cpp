@@ -163,7 +163,7 @@ struct DevBuf {
     size_t cap = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap) return 0;
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
         if (hipMalloc(&p, bytes) != hipSuccess) return fail(BCHK_ENOMEM, "hipMalloc(%zu) failed", bytes);
@@ -171,7 +171,7 @@ struct DevBuf {
         return 0;
     }
     void release() {
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
     }
@@ -199,8 +199,12 @@ struct bchk_ctx {
     int grid = 0;
     uint64_t max_decodes = 0;
     DevBuf y, res, l0, st, words, synd, ok;
+    // the cooperative kernel runs on `aux`, concurrently with the exact kernel
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool coop_concurrent = false;  // BCHK_COOP_CONCURRENT=1: measured neutral at 5 dB
     bool profile = false;
-    struct Ev { hipEvent_t e[4]; };
+    struct Ev { hipEvent_t e[6]; };  // [fast, exact, coop] x [start, end] of one call
     std::vector<Ev> events;
     double prof_ms[3] = {0.0, 0.0, 0.0};
     uint64_t prof_launches = 0;
@@ -215,17 +219,41 @@ int sigma_s2(int k, int n, double snr_db, double *sd) {
     return 0;
 }
 
-// control block: fast-path queue tail (line 0), 8 per-XCD heads (lines 1-8), heavy-queue
-// tail (line 9) and head (line 10); zeroed by one memset per decode call
-constexpr size_t kCtrlBytes = 11 * 128;
-constexpr int kHeavyTail = 32 * 9, kHeavyHead = 32 * 10;
+// control block: fast-path queue tail (line 0), 8 per-XCD heads (lines 1-8), heavy front
+// tail / head (lines 9, 10), back tail / head (11, 12), 8 per-XCD counts of codewords the
+// exact kernel has finished (13-20), diagnostic record count (21); zeroed by one memset
+// per decode call
+constexpr size_t kCtrlBytes = 22 * 128;
+constexpr int kHeavyTail = 32 * 9, kHeavyHead = 32 * 10, kHeavyTail2 = 32 * 11,
+              kHeavyHead2 = 32 * 12, kExactDone = 32 * 13;
+#ifdef BCHK_DIAG
+constexpr int kDiagCount = 32 * 21;
+#endif
+// a codeword handed to the cooperative kernel with a loop bound >= this goes to the front
+// queue (2^12 - 1: T >= 12 patterns left)
+constexpr uint64_t kHeavyBig = 4095;
 
+int ensure_heavy(bchk_ctx *c, size_t B) {
+    if (B <= c->heavy.cap / sizeof(uint32_t)) return 0;
+    int rc = c->heavy.ensure(B * sizeof(uint32_t));
+    if (rc) return rc;
+    // empty slots (consumers restore them after every read)
+    HIP_TRY(hipMemset(c->heavy.p, 0xFF, c->heavy.cap));
+    return 0;
+}
+
+// One decode call: the fast kernel on the launch stream, then the exact wave kernel on it
+// and -- concurrently, on the auxiliary stream -- the cooperative kernel, which takes heavy
+// codewords as soon as the exact kernel hands them off (longest first). The launch stream
+// waits for the cooperative kernel before the call's work counts as done.
 int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t *d_res,
                   double *d_l0, bchk_stats *d_st, hipStream_t s) {
     if (B == 0) return 0;
     if (B > 0xFFFFFFFFull) return fail(BCHK_EINVAL, "batch too large");
     int rc;
-    if ((rc = c->ctrl.ensure(kCtrlBytes)) || (rc = c->heavy.ensure(B * sizeof(uint32_t)))) return rc;
+    if ((rc = c->ctrl.ensure(kCtrlBytes)) || (rc = ensure_heavy(c, B))) return rc;
+    const bool fast = c->fast && c->use_fast;
+    if (fast && (rc = c->queue.ensure(B * sizeof(uint32_t)))) return rc;
     uint32_t *ctrl = (uint32_t *)c->ctrl.p;
     SearchParams p{};
     p.y = d_y;
@@ -242,22 +270,28 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     p.variant = variant;
     p.heavy_queue = (uint32_t *)c->heavy.p;
     p.heavy_tail = c->chunk_limit ? ctrl + kHeavyTail : nullptr;
+    p.heavy_tail2 = ctrl + kHeavyTail2;
     p.heavy_head = ctrl + kHeavyHead;
+    p.heavy_head2 = ctrl + kHeavyHead2;
+    p.exact_done = ctrl + kExactDone;
+    p.exact_total = fast ? ctrl : nullptr;  // the fast path's queue length
+    p.heavy_big = kHeavyBig;
     p.chunk_limit = c->chunk_limit;
 #ifdef BCHK_DIAG
     if (!c->diag.p) (void)c->diag.ensure(size_t(1) << 24);
     (void)hipMemsetAsync(c->diag.p, 0, size_t(1) << 24, s);
     p.diag = (unsigned long long *)c->diag.p;
+    p.diag_count = ctrl + kDiagCount;
 #endif
-
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    const bool conc = c->coop_concurrent && p.heavy_tail;
+    hipStream_t cs = conc ? c->aux : s;  // the cooperative kernel's stream
+    bchk_ctx::Ev ev{};
     if (c->profile) {
-        for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
-        HIP_TRY(hipEventRecord(ev[0], s));
+        for (auto &e : ev.e) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventRecord(ev.e[0], s));
     }
     HIP_TRY(hipMemsetAsync(ctrl, 0, kCtrlBytes, s));
-    if (c->fast && c->use_fast) {
-        if ((rc = c->queue.ensure(B * sizeof(uint32_t)))) return rc;
+    if (fast) {
         SearchParams f = p;
 #ifdef BCHK_DIAG
         f.diag = p.diag + (size_t(1) << 20);  // fast-kernel stamps: second half of the buffer
@@ -265,7 +299,14 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         f.qtail = ctrl;
         f.queue_out = (uint32_t *)c->queue.p;
         HIP_TRY(c->fast(f, c->lds_fast, s));
-        if (c->profile) HIP_TRY(hipEventRecord(ev[1], s));
+    }
+    if (c->profile) HIP_TRY(hipEventRecord(ev.e[1], s));
+    if (conc) {
+        HIP_TRY(hipEventRecord(c->ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(cs, c->ev_fork, 0));
+    }
+    if (c->profile) HIP_TRY(hipEventRecord(ev.e[2], s));
+    if (fast) {
         SearchParams q = p;
         q.queue = (const uint32_t *)c->queue.p;
         q.qcount = ctrl;
@@ -274,16 +315,22 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         HIP_TRY(launch_search(c->ks, q, c->grid, c->lds, s));
     } else {
         const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
-        const int grid = std::max(1, std::min(c->grid, need));
-        if (c->profile) HIP_TRY(hipEventRecord(ev[1], s));
-        HIP_TRY(launch_search(c->ks, p, grid, c->lds, s));
+        HIP_TRY(launch_search(c->ks, p, std::max(1, std::min(c->grid, need)), c->lds, s));
     }
-    if (c->profile) HIP_TRY(hipEventRecord(ev[2], s));
-    if (p.heavy_tail) HIP_TRY(c->ks.coop(p, c->grid_coop, c->lds_coop, s));
-    if (c->profile) {
-        HIP_TRY(hipEventRecord(ev[3], s));
-        c->events.push_back({{ev[0], ev[1], ev[2], ev[3]}});
+    if (c->profile) HIP_TRY(hipEventRecord(ev.e[3], s));
+    if (p.heavy_tail) {
+        if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));
+        HIP_TRY(c->ks.coop(p, c->grid_coop, c->lds_coop, cs));
+        if (c->profile) HIP_TRY(hipEventRecord(ev.e[5], cs));
+    } else if (c->profile) {
+        HIP_TRY(hipEventRecord(ev.e[4], s));
+        HIP_TRY(hipEventRecord(ev.e[5], s));
     }
+    if (conc) {
+        HIP_TRY(hipEventRecord(c->ev_join, cs));
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    }
+    if (c->profile) c->events.push_back(ev);
     return 0;
 }
 
@@ -331,7 +378,10 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     int rc = 0;
     if (hipMalloc(&c->d_tables, c->td.bytes) != hipSuccess ||
         hipMemcpy(c->d_tables, c->tables_host.data(), c->td.bytes, hipMemcpyHostToDevice) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         bchk_destroy(c);
         return fail(BCHK_EHIP, "device setup failed: %s", hipGetErrorString(hipGetLastError()));
     }
@@ -341,7 +391,15 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (select_fast(m, t, &c->fast)) c->lds_fast = tb + fast_block_waves() * fast_wave_bytes();
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);
+    if (const char *cc = getenv("BCHK_COOP_CONCURRENT")) c->coop_concurrent = atoi(cc) != 0;
     c->lds_coop = tb + c->ks.coop_bytes;
+    // one cooperative workgroup per CU by default (LDS sized past half the CU's 160 KB):
+    // a heavy codeword's 16 waves then own the CU's four SIMDs, which shortens the longest
+    // searches -- the critical path of a decode call -- and leaves the remaining wave slots
+    // to the concurrent exact kernel
+    int coop_target = 1;
+    if (const char *cp = getenv("BCHK_COOP_PER_CU")) coop_target = std::max(1, atoi(cp));
+    if (coop_target == 1) c->lds_coop = std::max<size_t>(c->lds_coop, 82 * 1024);
     const void *cfn = c->ks.coop_ptr();
     if (c->lds_coop > 65536)
         (void)hipFuncSetAttribute(cfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_coop);
@@ -354,7 +412,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     c->grid_coop = coop_per_cu * prop.multiProcessorCount;
     const void *fn = c->ks.search_ptr();
     if (c->lds > 65536)
-        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveSize * kWavesPerBlock, c->lds) != hipSuccess ||
         per_cu <= 0) {
@@ -381,8 +439,11 @@ void bchk_destroy(bchk_ctx *c) {
     c->words.release();
     c->synd.release();
     c->ok.release();
-    if (c->d_tables) hipFree(c->d_tables);
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->d_tables) (void)hipFree(c->d_tables);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -615,10 +676,11 @@ int bchk_profile(bchk_ctx *c, int enable) {
 int bchk_profile_read(bchk_ctx *c, double *ms3, uint64_t *launches) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
     for (auto &e : c->events) {
-        HIP_TRY(hipEventSynchronize(e.e[3]));
+        HIP_TRY(hipEventSynchronize(e.e[5]));
+        HIP_TRY(hipEventSynchronize(e.e[1]));
         for (int k = 0; k < 3; ++k) {
             float ms = 0.f;
-            HIP_TRY(hipEventElapsedTime(&ms, e.e[k], e.e[k + 1]));
+            HIP_TRY(hipEventElapsedTime(&ms, e.e[2 * k], e.e[2 * k + 1]));
             c->prof_ms[k] += ms;
         }
         c->prof_launches += 1;
@@ -635,12 +697,13 @@ int bchk_profile_read(bchk_ctx *c, double *ms3, uint64_t *launches) {
 
 int bchk_path_counts(bchk_ctx *c, uint64_t *to_exact, uint64_t *to_coop) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
-    uint32_t v[2] = {0, 0};
+    uint64_t v[2] = {0, 0};
     if (c->ctrl.p) {
-        HIP_TRY(hipMemcpyAsync(&v[0], (uint32_t *)c->ctrl.p, 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(&v[1], (uint32_t *)c->ctrl.p + kHeavyTail, 4, hipMemcpyDeviceToHost,
-                               c->stream));
+        std::vector<uint32_t> h(kCtrlBytes / 4);
+        HIP_TRY(hipMemcpyAsync(h.data(), c->ctrl.p, kCtrlBytes, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        v[0] = h[0];
+        v[1] = (uint64_t)h[kHeavyTail] + h[kHeavyTail2];
     }
     if (to_exact) *to_exact = v[0];
     if (to_coop) *to_coop = v[1];

@@ -336,7 +336,12 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         if (base >= S.bound) { S.i_end = S.bound; break; }
         if (p.max_decodes && base >= p.max_decodes) { S.i_end = base; S.truncated = true; break; }
         if (p.heavy_tail && chunks == p.chunk_limit) {
-            if (lane == 0) p.heavy_queue[atomicAdd(p.heavy_tail, 1u)] = cw;
+            if (lane == 0) {  // longest-first: large remaining bounds to the front queue
+                uint32_t *slot = S.bound >= p.heavy_big
+                                     ? p.heavy_queue + atomicAdd(p.heavy_tail, 1u)
+                                     : p.heavy_queue + (p.count - 1u - atomicAdd(p.heavy_tail2, 1u));
+                __hip_atomic_store(slot, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             return;  // redone from scratch by kaneko_coop_kernel
         }
         Mask<NW> diff;
@@ -369,6 +374,28 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     write_outputs<M, TMAX>(S, P, p, cw, lane);
 }
 
+// Relaxed device-scope atomics only: acquire/release at agent scope would write back or
+// invalidate this XCD's whole L2 on every use (L2s are not coherent across XCDs), and the
+// only data handed over are the atomic words themselves.
+__device__ __forceinline__ uint32_t ld_rlx(const uint32_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// s_waitcnt vmcnt(0): this wave's earlier memory operations (gfx9: loads and stores) have
+// completed before any later one issues; the asm is also a compiler barrier.
+__device__ __forceinline__ void mem_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// A wave of the exact kernel exits after `ndone` codewords (finished or handed off): it
+// adds them to its XCD's count (8 counters on separate lines: no single hot address). Its
+// hand-offs' tail increments have returned (their values addressed the slots) before the
+// count is issued, so a consumer that sees the counts complete sees final tails.
+__device__ __forceinline__ void wave_done(const SearchParams &p, int lane, uint32_t ndone) {
+    if (p.exact_done && lane == 0 && ndone) {
+        mem_drain();
+        __hip_atomic_fetch_add(p.exact_done + 32 * xcc_id(), ndone, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 template <int M, int TMAX>
 __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock)
 kaneko_search_kernel(SearchParams p) {
@@ -387,8 +414,10 @@ kaneko_search_kernel(SearchParams p) {
     uint8_t *ordl = wbase + NP * 16;
     if (!p.queue) {
         const uint32_t stride = gridDim.x * kWavesPerBlock;
-        for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride)
+        uint32_t ndone = 0;
+        for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride, ++ndone)
             search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ap, ordl, cw, lane);
+        wave_done(p, lane, ndone);
         return;
     }
     // Work queue left by the fast path: sub-queue x holds items x, x+8, x+16, ...; a wave
@@ -396,6 +425,7 @@ kaneko_search_kernel(SearchParams p) {
     const uint32_t total = *p.qcount;
     if ((blockIdx.x * kWavesPerBlock + wid) >= total) return;  // more waves than work
     int x = xcc_id();
+    uint32_t ndone = 0;
     for (int exhausted = 0; exhausted < 8;) {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(p.heads + 32 * x, 1u);
@@ -407,7 +437,9 @@ kaneko_search_kernel(SearchParams p) {
             continue;
         }
         search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane);
+        ++ndone;
     }
+    wave_done(p, lane, ndone);
 }
 
 // ---------------------------------------- cooperative search of heavy codewords
@@ -434,7 +466,8 @@ struct CoopCtl {
     uint32_t next;      // next chunk to hand out
     uint32_t consumed;  // chunks the acceptor has finished
     uint32_t done;      // the codeword's search has ended
-    uint32_t item;      // heavy-queue item of this workgroup
+    uint32_t item;      // the heavy codeword of this workgroup
+    uint32_t drec;      // diagnostic builds: its record index
     uint64_t bound;     // current loop bound (monotone non-increasing)
     double l0;          // current l0 (monotone non-increasing)
     uint32_t ready[kCoopSlots];  // chunk index + 1 once the slot holds that chunk
@@ -451,6 +484,49 @@ __device__ __forceinline__ uint64_t lds_ld64(const uint64_t *a) {
 }
 __device__ __forceinline__ void lds_st64(uint64_t *a, uint64_t v) {
     __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ uint32_t exact_finished(const SearchParams &p) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) v += ld_rlx(p.exact_done + 32 * x);
+    return v;
+}
+
+// Next heavy codeword for this workgroup (one thread), kEmptySlot when none is left. A
+// ticket of the front queue first: it is served as soon as the k-th big codeword is handed
+// off; once the exact kernel has finished and the front queue holds no k-th item, a ticket
+// of the back queue. One atomic per ticket (no compare-and-swap retries); every wait is
+// bounded, so a logic error ends the workgroup instead of hanging it.
+__device__ uint32_t next_heavy(const SearchParams &p) {
+    const uint32_t total = p.exact_total ? *p.exact_total : p.count;
+    for (int q = 0; q < 2; ++q) {
+        uint32_t *head = q ? p.heavy_head2 : p.heavy_head;
+        const uint32_t *tail = q ? p.heavy_tail2 : p.heavy_tail;
+        const uint32_t k = atomicAdd(head, 1u);
+        bool have = false;
+        for (uint32_t spins = 0; spins < kSpinLimit; ++spins) {
+            if (k < ld_rlx(tail)) { have = true; break; }
+            // the counts first (and waited for): if complete, the tail read after is final
+            const bool final = exact_finished(p) >= total;
+            mem_drain();
+            if (k < ld_rlx(tail)) { have = true; break; }
+            if (final) break;
+            __builtin_amdgcn_s_sleep(32);
+        }
+        if (!have) continue;
+        uint32_t *slot = q ? p.heavy_queue + (p.count - 1u - k) : p.heavy_queue + k;
+        for (uint32_t w = 0; w < kSpinLimit; ++w) {  // the producer stores after reserving
+            const uint32_t cw = ld_rlx(slot);
+            if (cw != kEmptySlot) {
+                __hip_atomic_store(slot, kEmptySlot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return cw;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return kEmptySlot;
+    }
+    return kEmptySlot;
 }
 
 template <int M, int TMAX>
@@ -473,12 +549,14 @@ kaneko_coop_kernel(SearchParams p) {
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
-    const uint32_t total = *p.heavy_tail;
     const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63) & ~63ull) : ~0ull;
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            ctl->item = atomicAdd(p.heavy_head, 1u);
+            ctl->item = next_heavy(p);
+#ifdef BCHK_DIAG
+            ctl->drec = atomicAdd(p.diag_count, 1u);
+#endif
             ctl->next = 0;
             ctl->consumed = 0;
             ctl->done = 0;
@@ -486,8 +564,11 @@ kaneko_coop_kernel(SearchParams p) {
         if (threadIdx.x < kCoopSlots) ctl->ready[threadIdx.x] = 0;
         __syncthreads();
         const uint32_t item = ctl->item;
-        if (item >= total) return;
-        const uint32_t cw = p.heavy_queue[item];
+        if (item == kEmptySlot) return;
+        const uint32_t cw = item;
+#ifdef BCHK_DIAG
+        const uint32_t drec = ctl->drec;  // this codeword's diagnostic record
+#endif
 #ifdef BCHK_DIAG
         // stamps (acceptor): [0] prep, [1] waiting for chunks, [2] acceptance, [3] chunks
         // decoded (all waves), [4] chunks accepted, [5] improvements, [6] total
@@ -648,12 +729,12 @@ kaneko_coop_kernel(SearchParams p) {
         }
 #ifdef BCHK_DIAG
         // chunk counts of every wave into the acceptor's record
-        if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long *>(&p.diag[(size_t)item * 8 + 3]), dg[3]);
+        if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long *>(&p.diag[(size_t)drec * 8 + 3]), dg[3]);
         if (wid == kAcceptor && lane == 0) {
             dg[6] = __builtin_amdgcn_s_memtime() - t_start;
             dg[7] = cw;
             for (int q = 0; q < 8; ++q)
-                if (q != 3) p.diag[(size_t)item * 8 + q] = dg[q];
+                if (q != 3) p.diag[(size_t)drec * 8 + q] = dg[q];
         }
 #endif
     }
@@ -697,21 +778,59 @@ __global__ void __launch_bounds__(256) alg_decode_kernel(AlgParams p) {
 
 // --------------------------------------------------------- FER counters
 // src/dataForPlot.cpp:55-74: frame errors, bit errors, decodes, comparisons, sums, words.
+// One wave per 64 rows: the rows' bytes are read as 16-B vectors (the 64-row block of
+// 64n bytes is contiguous and 16-B aligned when the arrays are), differing bytes -- rare at
+// the SNRs of interest -- are tallied per row in LDS, then lane r owns row r.
 template <int N>
 __global__ void __launch_bounds__(256) count_kernel(const uint8_t *tx, const uint8_t *res,
                                                     const bchk_stats *st, uint32_t B,
                                                     unsigned long long *out6) {
+    __shared__ uint32_t rowerr[4][64];
     __shared__ unsigned long long part[6][4];
-    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
-    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) {
-        int be = 0;
-        for (int i = 0; i < N; ++i) be += tx[(size_t)b * N + i] != res[(size_t)b * N + i];
-        c[0] += be ? 1 : 0;
-        c[1] += be;
-        if (st) { c[2] += st[b].decodes; c[3] += st[b].comparisons; c[4] += st[b].sums; }
-        c[5] += 1;
-    }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
+    const bool vec = ((reinterpret_cast<uintptr_t>(tx) | reinterpret_cast<uintptr_t>(res)) & 15u) == 0;
+    const uint32_t stride = gridDim.x * 4u * 64u;
+    for (uint32_t r0 = (blockIdx.x * 4u + (uint32_t)wid) * 64u; r0 < B; r0 += stride) {
+        rowerr[wid][lane] = 0;
+        wave_sync();
+        const uint32_t rows = (B - r0) < 64u ? (B - r0) : 64u;
+        const size_t base = (size_t)r0 * N;
+        const uint32_t bytes = rows * (uint32_t)N;
+        if (vec && rows == 64u) {  // 64 N bytes = 4 N vectors
+            const uint4 *a4 = reinterpret_cast<const uint4 *>(tx + base);
+            const uint4 *b4 = reinterpret_cast<const uint4 *>(res + base);
+            for (uint32_t v = (uint32_t)lane; v < 4u * N; v += 64u) {
+                const uint4 a = a4[v], b = b4[v];
+                const uint32_t x[4] = {a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (!x[k]) continue;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if ((x[k] >> (8 * q)) & 0xFFu)
+                            atomicAdd(&rowerr[wid][(16u * v + 4u * k + q) / N], 1u);
+                }
+            }
+        } else {
+            for (uint32_t o = (uint32_t)lane; o < bytes; o += 64u)
+                if (tx[base + o] != res[base + o]) atomicAdd(&rowerr[wid][o / N], 1u);
+        }
+        wave_sync();
+        if ((uint32_t)lane < rows) {
+            const uint32_t e = rowerr[wid][lane];
+            c[0] += e ? 1 : 0;
+            c[1] += e;
+            if (st) {
+                const bchk_stats &s = st[r0 + lane];
+                c[2] += s.decodes;
+                c[3] += s.comparisons;
+                c[4] += s.sums;
+            }
+            c[5] += 1;
+        }
+        wave_sync();
+    }
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         unsigned long long v = c[k];
@@ -783,7 +902,7 @@ hipError_t launch_alg(const KernelSet &k, const AlgParams &p, size_t lds, hipStr
 }
 hipError_t launch_count(int n, const uint8_t *tx, const uint8_t *res, const bchk_stats *st,
                         uint32_t B, uint64_t *out6, hipStream_t s) {
-    const int grid = (int)((B + 255) / 256) < 2048 ? (int)((B + 255) / 256) : 2048;
+    const int grid = (int)((B + 255) / 256) < 16384 ? (int)((B + 255) / 256) : 16384;
     unsigned long long *o = reinterpret_cast<unsigned long long *>(out6);
     switch (n) {
 #define BCHK_CNT(NN) \
