@@ -139,6 +139,20 @@ int bchk_path_counts(bchk_ctx *ctx, uint64_t *to_exact, uint64_t *to_coop);
 /* Enable (default) or disable the fast path; results are identical either way. */
 int bchk_set_fast_path(bchk_ctx *ctx, int enable);
 
+/* Enable (default) or disable the syndrome decoding table of the search kernels: for
+ * n <= 63 and m (t - 1) <= 30, Decoder::decode of a test pattern is a lookup of its
+ * normalised syndrome in a table of the weight <= t coset leaders (csrc/bchk_syndtab.h)
+ * instead of Berlekamp-Massey + Chien. Results are identical either way. */
+int bchk_set_syndrome_table(bchk_ctx *ctx, int enable);
+/* Host-side decode through that table (no GPU): for odd syndromes synd[i][0..t) =
+ * S_1, S_3, ..., S_{2t-1}, ok[i] = 1 iff Decoder::decode succeeds, and err[i] (may be
+ * NULL) = the flipped positions as a bit mask. BCHK_EINVAL when (m, t) has no table.
+ * Test/diagnostic entry point. */
+int bchk_syndrome_table_query(int m, int t, const uint32_t *synd, size_t N, uint8_t *ok,
+                              uint64_t *err);
+/* Size of that table: distinct keys, bytes, longest probe sequence (buckets). */
+int bchk_syndrome_table_info(int m, int t, uint64_t *keys, uint64_t *bytes, uint32_t *max_probe);
+
 const char *bchk_last_error(void);
 const char *bchk_version(void);
 

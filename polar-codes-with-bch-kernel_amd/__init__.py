@@ -32,7 +32,8 @@ EXPORTS = (
     "bchk_set_max_decodes", "bchk_decode_host", "bchk_decode_device",
     "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device",
     "bchk_generate_host", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
-    "bchk_profile_read", "bchk_path_counts", "bchk_set_fast_path", "bchk_last_error", "bchk_version",
+    "bchk_profile_read", "bchk_path_counts", "bchk_set_fast_path", "bchk_set_syndrome_table",
+    "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_last_error", "bchk_version",
 )
 
 STATS_DTYPE = np.dtype([("decodes", "<u8"), ("comparisons", "<u8"), ("sums", "<u8"),
@@ -89,6 +90,10 @@ def lib():
     L.bchk_profile.argtypes = [vp, i32]
     L.bchk_profile_read.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
     L.bchk_set_fast_path.argtypes = [vp, i32]
+    L.bchk_set_syndrome_table.argtypes = [vp, i32]
+    L.bchk_syndrome_table_query.argtypes = [i32, i32, vp, sz, vp, vp]
+    L.bchk_syndrome_table_info.argtypes = [i32, i32, C.POINTER(u64), C.POINTER(u64),
+                                           C.POINTER(C.c_uint32)]
     L.bchk_path_counts.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)]
     L.bchk_last_error.restype = C.c_char_p
     L.bchk_version.restype = C.c_char_p
@@ -216,6 +221,28 @@ class KanekoKernelProcessor:
 
     def set_fast_path(self, enable=True):
         _check(lib().bchk_set_fast_path(self._h, 1 if enable else 0))
+
+    def set_syndrome_table(self, enable=True):
+        """Syndrome decoding table of the search kernels (results identical either way)."""
+        _check(lib().bchk_set_syndrome_table(self._h, 1 if enable else 0))
+
+
+def syndrome_table_query(m, t, syndromes):
+    """Host-side Decoder::decode through the syndrome table (no GPU): syndromes [N][t] odd
+    syndromes S_1, S_3, ... as uint32 -> (ok [N] bool, flipped-position masks [N] uint64)."""
+    syn = np.ascontiguousarray(syndromes, np.uint32)
+    N = syn.shape[0]
+    ok = np.zeros(N, np.uint8)
+    err = np.zeros(N, np.uint64)
+    _check(lib().bchk_syndrome_table_query(m, t, _p(syn), N, _p(ok), _p(err)))
+    return ok.astype(bool), err
+
+
+def syndrome_table_info(m, t):
+    """(distinct keys, bytes, longest probe sequence) of the (m, t) syndrome table."""
+    k, b, p = C.c_uint64(), C.c_uint64(), C.c_uint32()
+    _check(lib().bchk_syndrome_table_info(m, t, C.byref(k), C.byref(b), C.byref(p)))
+    return k.value, b.value, p.value
 
 
 def version():

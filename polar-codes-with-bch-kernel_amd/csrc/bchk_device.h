@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "bchk.h"
+#include "bchk_syndtab.h"
 
 namespace bchk {
 
@@ -69,6 +70,9 @@ struct SearchParams {
     // diagnostic builds only (-DBCHK_DIAG): per heavy-queue item, 8 u64 timing counters
     unsigned long long *diag;
     uint32_t *diag_count;
+    // syndrome-indexed decoding table (bchk_syndtab.h) for the search kernels' test
+    // patterns; slots == null: Berlekamp-Massey + Chien
+    SyndTable tab;
     int32_t t;
     int32_t J;             // < 0: shipped
     int32_t variant;       // BCHK_VARIANT_*

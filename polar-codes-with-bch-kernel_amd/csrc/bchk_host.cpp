@@ -15,7 +15,9 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <random>
+#include <thread>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -177,6 +179,172 @@ struct DevBuf {
     }
 };
 
+// ------------------------------------------------------ syndrome decoding table
+// Host build of the table described in bchk_syndtab.h. Every error pattern of weight 1..t
+// that contains position 0 is enumerated (incremental odd-syndrome XOR over the position
+// columns); its normalised key maps to the pattern shifted by the normalising shift (the
+// same entry for every member of a shift orbit: inserted once). Keys in the raw region
+// (all coprime syndromes zero, no normalisation) are inserted for all n cyclic shifts.
+typedef SyndKey (*SyndKeyFn)(const uint32_t *, int, const uint16_t *, const uint8_t *);
+constexpr int kTabTmax = 8;  // t <= 7 whenever syndtab_feasible(m, t)
+
+SyndKeyFn synd_key_fn(int m) {
+    switch (m) {
+        case 2: return &synd_key<2, kTabTmax>;
+        case 3: return &synd_key<3, kTabTmax>;
+        case 4: return &synd_key<4, kTabTmax>;
+        case 5: return &synd_key<5, kTabTmax>;
+        case 6: return &synd_key<6, kTabTmax>;
+        default: return nullptr;
+    }
+}
+
+struct HostTable {
+    int m = 0, t = 0;
+    uint32_t bbits = 0, max_probe = 0;
+    size_t keys = 0;
+    std::vector<uint64_t> slots;  // [nbuckets][kTabSlots][2]
+};
+
+uint64_t rotl_mask(uint64_t v, int s, int n) {
+    const uint64_t full = (n == 64) ? ~0ull : ((1ull << n) - 1ull);
+    return s ? (((v << s) | (v >> (n - s))) & full) : v;
+}
+
+// Insert (key, mask) unless the key is present (then the mask must agree: the coset
+// leader is unique). Returns false on a disagreement (a logic error).
+bool tab_insert(HostTable &h, uint64_t key, uint64_t mask) {
+    const uint32_t bm = (1u << h.bbits) - 1u;
+    uint32_t b = tab_hash(key, h.bbits);
+    for (uint32_t p = 0;; ++p) {
+        uint64_t *bk = h.slots.data() + (size_t)b * (2 * kTabSlots);
+        for (int j = 0; j < kTabSlots; ++j) {
+            if (bk[2 * j] == key) return bk[2 * j + 1] == mask;
+            if (bk[2 * j] == 0) {
+                bk[2 * j] = key;
+                bk[2 * j + 1] = mask;
+                h.max_probe = std::max(h.max_probe, p + 1);
+                ++h.keys;
+                return true;
+            }
+        }
+        b = (b + 1u) & bm;
+    }
+}
+
+int build_table(const Field &f, int t, HostTable &h) {
+    const int m = f.m, n = f.n;
+    h.m = m;
+    h.t = t;
+    TableDesc td{};
+    const std::vector<uint8_t> blob = make_tables(f, t, &td);
+    const uint8_t *ex = blob.data() + td.off_exp;
+    const uint16_t *lg = reinterpret_cast<const uint16_t *>(blob.data() + td.off_log);
+    std::vector<uint64_t> col(n, 0);  // packed odd-syndrome column of each position
+    for (int p = 0; p < n; ++p)
+        for (int q = 0; q < t; ++q)
+            col[p] |= uint64_t(f.alog[(size_t(2 * q + 1) * p) % n]) << (8 * q);
+    const SyndKeyFn keyf = synd_key_fn(m);
+    // raw-region keys: every coprime syndrome zero (the key's region is the last one)
+    int K = 0;
+    for (int q = 0; q < t; ++q) K += f_coprime(q, n) ? 1 : 0;
+    // table size: <= 30 % of slots used (orbits ~ C(n, <=t) / n, plus raw-region keys)
+    double est = 0.0, c = 1.0;
+    for (int w = 1; w <= t; ++w) {
+        c = c * (n - w + 1) / w;
+        est += c;
+    }
+    est = est / n + 64;
+    h.bbits = 1;
+    while ((double)(kTabSlots << h.bbits) * 0.3 < est) ++h.bbits;
+    h.slots.assign((size_t(kTabSlots) << h.bbits) * 2, 0);
+    // enumerate in parallel (threads own second positions), insert serially
+    const int hw = (int)std::thread::hardware_concurrency();
+    const int nth = std::max(1, std::min(16, hw > 0 ? hw : 1));
+    std::vector<std::vector<uint64_t>> found(nth);  // (key, mask) pairs
+    auto emit = [&](std::vector<uint64_t> &out, uint64_t S, uint64_t pat) {
+        const uint32_t Sw[2] = {(uint32_t)S, (uint32_t)(S >> 32)};
+        const SyndKey k = keyf(Sw, t, lg, ex);
+        if (((k.key - 1) >> 32) < (uint64_t)K) {  // a normalised region
+            out.push_back(k.key);
+            out.push_back(rotl_mask(pat, k.s, n));  // the pattern shifted by +s
+            return;
+        }
+        for (int u = 0; u < n; ++u) {  // raw region: each shift is its own key
+            uint64_t Su = 0;
+            for (int q = 0; q < t; ++q) {
+                const unsigned v = (S >> (8 * q)) & 0xFFu;
+                const unsigned w = v ? f.alog[(f.log[v] + size_t(2 * q + 1) * u) % n] : 0u;
+                Su |= uint64_t(w) << (8 * q);
+            }
+            const uint32_t Swu[2] = {(uint32_t)Su, (uint32_t)(Su >> 32)};
+            out.push_back(keyf(Swu, t, lg, ex).key);
+            out.push_back(rotl_mask(pat, u, n));
+        }
+    };
+    struct Rec {
+        const std::vector<uint64_t> &col;
+        int n;
+        const decltype(emit) &put;
+        void go(std::vector<uint64_t> &out, int from, int left, uint64_t S, uint64_t pat) const {
+            for (int p = from; p < n; ++p) {
+                const uint64_t Sp = S ^ col[p], pp = pat | (1ull << p);
+                put(out, Sp, pp);
+                if (left > 1) go(out, p + 1, left - 1, Sp, pp);
+            }
+        }
+    };
+    const Rec rec{col, n, emit};
+    std::vector<std::thread> th;
+    for (int w = 0; w < nth; ++w)
+        th.emplace_back([&, w] {
+            if (w == 0) emit(found[0], col[0], 1ull);  // weight 1: {0}
+            for (int p1 = 1 + w; p1 < n && t >= 2; p1 += nth) {
+                const uint64_t S1 = col[0] ^ col[p1], pat = 1ull | (1ull << p1);
+                emit(found[w], S1, pat);
+                if (t > 2) rec.go(found[w], p1 + 1, t - 2, S1, pat);
+            }
+        });
+    for (auto &x : th) x.join();
+    for (auto &v : found) {
+        for (size_t i = 0; i < v.size(); i += 2)
+            if (!tab_insert(h, v[i], v[i + 1]))
+                return fail(BCHK_EINVAL, "syndrome table: two leaders for one key (m=%d t=%d)", m, t);
+        std::vector<uint64_t>().swap(v);
+    }
+    return 0;
+}
+
+// Process-wide cache: one host table per (m, t), one device copy per (device, m, t).
+struct TableCache {
+    std::mutex mu;
+    std::vector<HostTable *> host;
+    struct Dev { int device, m, t; uint64_t *slots; };
+    std::vector<Dev> dev;
+};
+TableCache &table_cache() {
+    static TableCache *c = new TableCache();  // never destroyed (outlives static dtors)
+    return *c;
+}
+
+int host_table(const Field &f, int t, const HostTable **out) {
+    TableCache &tc = table_cache();
+    std::lock_guard<std::mutex> g(tc.mu);
+    for (auto *h : tc.host)
+        if (h->m == f.m && h->t == t) {
+            *out = h;
+            return 0;
+        }
+    auto *h = new HostTable();
+    if (int rc = build_table(f, t, *h)) {
+        delete h;
+        return rc;
+    }
+    tc.host.push_back(h);
+    *out = h;
+    return 0;
+}
+
 }  // namespace
 
 struct bchk_ctx {
@@ -204,6 +372,9 @@ struct bchk_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool coop_concurrent = false;  // BCHK_COOP_CONCURRENT=1: measured neutral at 5 dB
     bool profile = false;
+    // syndrome decoding table (bchk_syndtab.h): built on first use, shared across contexts
+    bool use_table = true;
+    SyndTable tab{};
     struct Ev { hipEvent_t e[6]; };  // [fast, exact, coop] x [start, end] of one call
     std::vector<Ev> events;
     double prof_ms[3] = {0.0, 0.0, 0.0};
@@ -242,6 +413,32 @@ int ensure_heavy(bchk_ctx *c, size_t B) {
     return 0;
 }
 
+// The context's device copy of the syndrome decoding table (first decode call; no-op when
+// (m, t) has none or it is disabled).
+int ensure_table(bchk_ctx *c) {
+    if (!c->use_table || c->tab.slots || !syndtab_feasible(c->m, c->t)) return 0;
+    const HostTable *h = nullptr;
+    if (int rc = host_table(c->field, c->t, &h)) return rc;
+    TableCache &tc = table_cache();
+    std::lock_guard<std::mutex> g(tc.mu);
+    uint64_t *d = nullptr;
+    for (auto &e : tc.dev)
+        if (e.device == c->device && e.m == c->m && e.t == c->t) d = e.slots;
+    if (!d) {
+        const size_t bytes = h->slots.size() * sizeof(uint64_t);
+        if (hipMalloc(&d, bytes) != hipSuccess) return fail(BCHK_ENOMEM, "hipMalloc(%zu) for the syndrome table", bytes);
+        if (hipMemcpy(d, h->slots.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return fail(BCHK_EHIP, "syndrome table upload failed");
+        }
+        tc.dev.push_back({c->device, c->m, c->t, d});
+    }
+    c->tab.slots = d;
+    c->tab.bbits = h->bbits;
+    c->tab.max_probe = h->max_probe;
+    return 0;
+}
+
 // One decode call: the fast kernel on the launch stream, then the exact wave kernel on it
 // and -- concurrently, on the auxiliary stream -- the cooperative kernel, which takes heavy
 // codewords as soon as the exact kernel hands them off (longest first). The launch stream
@@ -254,6 +451,7 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     if ((rc = c->ctrl.ensure(kCtrlBytes)) || (rc = ensure_heavy(c, B))) return rc;
     const bool fast = c->fast && c->use_fast;
     if (fast && (rc = c->queue.ensure(B * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure_table(c))) return rc;
     uint32_t *ctrl = (uint32_t *)c->ctrl.p;
     SearchParams p{};
     p.y = d_y;
@@ -277,6 +475,7 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     p.exact_total = fast ? ctrl : nullptr;  // the fast path's queue length
     p.heavy_big = kHeavyBig;
     p.chunk_limit = c->chunk_limit;
+    if (c->use_table) p.tab = c->tab;
 #ifdef BCHK_DIAG
     if (!c->diag.p) (void)c->diag.ensure(size_t(1) << 24);
     (void)hipMemsetAsync(c->diag.p, 0, size_t(1) << 24, s);
@@ -390,6 +589,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     c->lds_alg = tb;
     if (select_fast(m, t, &c->fast)) c->lds_fast = tb + fast_block_waves() * fast_wave_bytes();
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
+    if (getenv("BCHK_NO_TABLE")) c->use_table = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);
     if (const char *cc = getenv("BCHK_COOP_CONCURRENT")) c->coop_concurrent = atoi(cc) != 0;
     c->lds_coop = tb + c->ks.coop_bytes;
@@ -720,6 +920,55 @@ int bchk_diag_read(bchk_ctx *c, uint64_t *out, size_t items) {
     return 0;
 }
 #endif
+
+int bchk_set_syndrome_table(bchk_ctx *c, int enable) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    c->use_table = enable != 0;
+    return 0;
+}
+
+int bchk_syndrome_table_query(int m, int t, const uint32_t *synd, size_t N, uint8_t *ok,
+                              uint64_t *err) {
+    if (N && (!synd || !ok)) return fail(BCHK_EINVAL, "NULL argument");
+    if (m < 2 || m > kMaxM || t < 1 || t >= (1 << (m - 1))) return fail(BCHK_EINVAL, "bad m/t");
+    if (!syndtab_feasible(m, t)) return fail(BCHK_EINVAL, "no syndrome table for m=%d t=%d", m, t);
+    const Field f = make_field(m);
+    const HostTable *h = nullptr;
+    if (int rc = host_table(f, t, &h)) return rc;
+    TableDesc td{};
+    const std::vector<uint8_t> blob = make_tables(f, t, &td);
+    const uint8_t *ex = blob.data() + td.off_exp;
+    const uint16_t *lg = reinterpret_cast<const uint16_t *>(blob.data() + td.off_log);
+    SyndTable T{h->slots.data(), h->bbits, h->max_probe};
+    for (size_t i = 0; i < N; ++i) {
+        uint32_t Sw[2] = {0, 0};
+        for (int q = 0; q < t; ++q) Sw[q >> 2] |= (synd[i * t + q] & 0xFFu) << (8 * (q & 3));
+        uint64_t E = 0;
+        bool hit = false;
+        switch (m) {
+            case 2: hit = tab_decode<2, kTabTmax>(T, Sw, t, lg, ex, E); break;
+            case 3: hit = tab_decode<3, kTabTmax>(T, Sw, t, lg, ex, E); break;
+            case 4: hit = tab_decode<4, kTabTmax>(T, Sw, t, lg, ex, E); break;
+            case 5: hit = tab_decode<5, kTabTmax>(T, Sw, t, lg, ex, E); break;
+            default: hit = tab_decode<6, kTabTmax>(T, Sw, t, lg, ex, E); break;
+        }
+        ok[i] = hit ? 1 : 0;
+        if (err) err[i] = E;
+    }
+    return 0;
+}
+
+int bchk_syndrome_table_info(int m, int t, uint64_t *keys, uint64_t *bytes, uint32_t *max_probe) {
+    if (!syndtab_feasible(m, t) || t >= (1 << (m - 1)))
+        return fail(BCHK_EINVAL, "no syndrome table for m=%d t=%d", m, t);
+    const Field f = make_field(m);
+    const HostTable *h = nullptr;
+    if (int rc = host_table(f, t, &h)) return rc;
+    if (keys) *keys = h->keys;
+    if (bytes) *bytes = h->slots.size() * sizeof(uint64_t);
+    if (max_probe) *max_probe = h->max_probe;
+    return 0;
+}
 
 int bchk_set_fast_path(bchk_ctx *c, int enable) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");

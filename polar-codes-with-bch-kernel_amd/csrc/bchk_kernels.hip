@@ -154,6 +154,7 @@ template <int M, int TMAX>
 __device__ __forceinline__ bool decode_chunk(const Prep<M, TMAX> &P, uint64_t base, int t,
                                              const uint8_t *ex, const uint16_t *lg,
                                              const uint64_t *chien, const double *ap,
+                                             const SyndTable &T,
                                              Mask<Geo<M>::NW> &diff, int &m, double &l) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
     constexpr int NB = N < 31 ? N : 31;
@@ -170,7 +171,17 @@ __device__ __forceinline__ bool decode_chunk(const Prep<M, TMAX> &P, uint64_t ba
         mask_set<NW>(Pm, pb);
     }
     Mask<NW> E;
-    const bool ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, t, E);
+    bool ok;
+    if constexpr (M <= 6 && TMAX <= 8) {
+        if (T.slots) {
+            // the decoder as a table lookup (bchk_syndtab.h): identical result
+            ok = tab_decode<M, TMAX>(T, Sw, t, lg, ex, E.w[0]);
+        } else {
+            ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, t, E);
+        }
+    } else {
+        ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, t, E);
+    }
 #pragma unroll
     for (int s = 0; s < NW; ++s) diff.w[s] = Pm.w[s] ^ E.w[s];
     m = 0;
@@ -347,14 +358,15 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         Mask<NW> diff;
         int m;
         double l;
-        const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, diff, m, l);
-        const bool live = ok && base + (uint64_t)lane < S.bound;
-        const uint64_t okm = ballot(live);
+        const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, p.tab, diff, m, l);
+        const uint64_t okm = ballot(ok);
         if (base == 0 && !(okm & 1ull)) S.firstOK = false;  // :371
         // Only improvements (l < l0) change the state: m0 at an improvement is the fixed
         // i = 0 value or, once i = 0 has failed, the improving candidate's own m (:374), and
-        // l0 only decreases, so successes with l >= l0 can be skipped wholesale.
-        uint64_t imp = ballot(live && l < S.l0);
+        // l0 only decreases, so successes with l >= l0 can be skipped wholesale. The loop
+        // bound is NOT monotone (T comes from the calcT scan of each improvement, and
+        // (1 << T) - 1 wraps at 32 bits), so lanes are tested against the current bound.
+        uint64_t imp = ballot(ok && l < S.l0);
         while (imp) {
             const int L = (int)__builtin_ctzll(imp);
             const uint64_t ii = base + (uint64_t)L;
@@ -367,7 +379,7 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
             accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
             if (S.done) break;
             // l0 dropped: re-filter the later lanes of this chunk
-            imp = ballot(live && l < S.l0) & ~((2ull << L) - 1ull);
+            imp = ballot(ok && l < S.l0) & ~((2ull << L) - 1ull);
         }
         if (S.done) break;
     }
@@ -468,7 +480,7 @@ struct CoopCtl {
     uint32_t done;      // the codeword's search has ended
     uint32_t item;      // the heavy codeword of this workgroup
     uint32_t drec;      // diagnostic builds: its record index
-    uint64_t bound;     // current loop bound (monotone non-increasing)
+    uint64_t bound;     // the acceptor's current loop bound (diagnostics; may rise again)
     double l0;          // current l0 (monotone non-increasing)
     uint32_t ready[kCoopSlots];  // chunk index + 1 once the slot holds that chunk
 };
@@ -595,8 +607,10 @@ kaneko_coop_kernel(SearchParams p) {
                 if (lane == 0) c = atomicAdd(&ctl->next, 1u);
                 c = (uint32_t)__shfl((int)c, 0, 64);
                 const uint64_t base = 64ull * c;
-                uint64_t bound = lds_ld64(&ctl->bound);
-                if (base >= bound || base >= capc || lds_ld(&ctl->done)) break;
+                // no early stop on the published loop bound: it can rise again after a later
+                // improvement (T is not monotone), so only the acceptor decides the end; the
+                // ring keeps decoders at most kCoopSlots chunks ahead of it
+                if (base >= capc || lds_ld(&ctl->done)) break;
                 // the slot is free once the acceptor has finished chunk c - kCoopSlots
                 bool stop = false;
                 for (uint32_t spins = 0; c >= lds_ld(&ctl->consumed) + kCoopSlots; ++spins) {
@@ -604,19 +618,17 @@ kaneko_coop_kernel(SearchParams p) {
                     __builtin_amdgcn_s_sleep(2);
                 }
                 if (stop) break;
-                bound = lds_ld64(&ctl->bound);
                 const double l0r = __longlong_as_double((long long)lds_ld64(
                     reinterpret_cast<const uint64_t *>(&ctl->l0)));
                 Mask<NW> diff;
                 int m;
                 double l;
-                const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, diff, m, l);
-                const bool live = ok && base + (uint64_t)lane < bound;
+                const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, p.tab, diff, m, l);
                 const uint64_t okm = ballot(ok);
                 // candidates: the strict running minima of l over this chunk's successes,
                 // below l0 as last published. The improvements are the running minima over
                 // all successes in pattern order, so they are a subset of these.
-                const uint64_t cm = ballot(live && l < l0r);
+                const uint64_t cm = ballot(ok && l < l0r);
                 uint64_t cand = 0;
                 double run = l0r;
                 for (uint64_t mm = cm; mm; mm &= mm - 1) {

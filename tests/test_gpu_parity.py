@@ -20,15 +20,19 @@ _ctx = {}
 #                      workgroup-cooperative kernel after 4 chunks
 #   "exact-only"       no fast path, no cooperative hand-off (one wave per codeword)
 #   "coop-heavy"       cooperative hand-off after the first chunk
-PATHS = {"fast+exact+coop": (True, None), "exact-only": (False, "0"), "coop-heavy": (True, "1")}
+#   "no-table"         default paths with Berlekamp-Massey + Chien for every test pattern
+#                      instead of the syndrome decoding table (csrc/bchk_syndtab.h)
+PATHS = {"fast+exact+coop": (True, None, True), "exact-only": (False, "0", True),
+         "coop-heavy": (True, "1", True), "no-table": (True, None, False)}
 
 
 def dec(m, t, J=-1, fast=True, path=None):
+    filt = True
     if path is not None:
-        fast, limit = PATHS[path]
+        fast, limit, filt = PATHS[path]
     else:
         limit = None
-    key = (m, t, J, fast, limit)
+    key = (m, t, J, fast, limit, filt)
     if key not in _ctx:
         old = os.environ.pop("BCHK_CHUNK_LIMIT", None)
         if limit is not None:
@@ -40,6 +44,7 @@ def dec(m, t, J=-1, fast=True, path=None):
             if old is not None:
                 os.environ["BCHK_CHUNK_LIMIT"] = old
         d.set_fast_path(fast)
+        d.set_syndrome_table(filt)
         _ctx[key] = d
     return _ctx[key]
 
@@ -245,3 +250,72 @@ def test_path_counts_and_profile_report_each_stage():
     to_exact, to_coop = d.path_counts()
     assert calls == 1 and len(ms) == 3 and ms[0] > 0 and ms[1] > 0
     assert 0 < to_exact < (1 << 14) and 0 < to_coop <= to_exact
+
+
+@pytest.mark.parametrize("m,t", [(4, 2), (5, 3), (6, 6), (6, 4), (5, 7)])
+def test_syndrome_table_agrees_with_gpu_decoder(m, t):
+    # table decode == the GPU Berlekamp-Massey + Chien decoder (itself pinned to the
+    # reference's decoder tables): random syndromes, plus ones steered into every key region
+    # (leading coprime syndromes zero) and syndromes of low-weight patterns
+    F = load()
+    rng = np.random.default_rng(7 * m + t)
+    S = rng.integers(0, 1 << m, (6000, t)).astype(np.uint32)
+    S[1000:2000, 0] = 0
+    S[2000:3000, :min(t, 3)] = 0
+    S[3000:3500, :] = 0
+    S[3500:3600, 1:] = 0
+    o = Oracle(m, t)
+    n = o.n
+    for b in range(3600, 6000):
+        pos = rng.choice(n, size=int(rng.integers(1, t + 2)), replace=False)
+        for q in range(t):
+            v = 0
+            for p in pos:
+                v ^= o.code.alog[((2 * q + 1) * int(p)) % n]
+            S[b, q] = v
+    ok, ans = dec(m, t).alg_decode(np.zeros((len(S), n), np.uint8), syndromes=S)
+    hit, err = F.syndrome_table_query(m, t, S)
+    np.testing.assert_array_equal(hit, ok)
+    bits = (err[ok][:, None] >> np.arange(n, dtype=np.uint64)) & np.uint64(1)
+    np.testing.assert_array_equal(bits.astype(np.uint8), ans[ok])
+    assert ok.sum() > 100
+
+
+@pytest.mark.parametrize("m,t,J,snr,B", [(6, 6, 15, 3.0, 4096), (6, 6, -1, 5.0, 1024),
+                                         (5, 3, -1, 2.0, 8192), (4, 2, 15, 1.0, 8192)])
+def test_syndrome_table_on_off_identical(m, t, J, snr, B):
+    on, off = dec(m, t, J=J), dec(m, t, J=J, path="no-table")
+    _, y, _ = on.generate(snr, B, seed=404)
+    on.set_max_decodes(1 << 21)
+    off.set_max_decodes(1 << 21)
+    a, b = on.decode(y), off.decode(y)
+    on.set_max_decodes(0)
+    off.set_max_decodes(0)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+    np.testing.assert_array_equal(a[2], b[2])
+
+
+def test_uncapped_batch_all_paths_agree_and_match_oracle():
+    # J = inf at 5 dB over the full headline batch: the loop bound (1 << T) - 1 is not
+    # monotone (T from each improvement's calcT scan, 32-bit wrap), so a cooperative
+    # decoder must never stop on a bound it has seen -- codeword 55257 of this stream
+    # lowers its bound and raises it again. Every path, no truncation, oracle on the
+    # heavy rows.
+    F = load()
+    ds = [dec(6, 6, J=-1, path=p) for p in PATHS]
+    _, y, _ = ds[0].generate(5.0, 1 << 20, seed=1)
+    ref = ds[0].decode(y)
+    assert not np.any(ref[2]["flags"] & F.F_TRUNCATED)
+    for d in ds[1:]:
+        b = d.decode(y)
+        np.testing.assert_array_equal(ref[0], b[0])
+        np.testing.assert_array_equal(ref[1].view(np.uint64), b[1].view(np.uint64))
+        np.testing.assert_array_equal(ref[2], b[2])
+    decs = ref[2]["decodes"].astype(np.int64)
+    heavy = np.flatnonzero((decs > 64) & (decs <= 140000))
+    rows = np.unique(np.concatenate([[55257], np.random.default_rng(2).choice(heavy, 24)]))
+    o = Oracle(6, 6)
+    r2, l2, s2, a2 = o.kaneko_batch(y[rows], J=-1)
+    res, l0, st = ref[0][rows], ref[1][rows], ref[2][rows]
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, res, l0, st)
