@@ -185,7 +185,7 @@ struct DevBuf {
 // columns); its normalised key maps to the pattern shifted by the normalising shift (the
 // same entry for every member of a shift orbit: inserted once). Keys in the raw region
 // (all coprime syndromes zero, no normalisation) are inserted for all n cyclic shifts.
-typedef SyndKey (*SyndKeyFn)(const uint32_t *, int, const uint16_t *, const uint8_t *);
+typedef SyndKey (*SyndKeyFn)(const uint32_t *, int, const uint16_t *);
 constexpr int kTabTmax = 8;  // t <= 7 whenever syndtab_feasible(m, t)
 
 SyndKeyFn synd_key_fn(int m) {
@@ -206,12 +206,22 @@ struct HostTable {
     std::vector<uint64_t> slots;  // [nbuckets][kTabSlots][2]
 };
 
-uint64_t rotl_mask(uint64_t v, int s, int n) {
-    const uint64_t full = (n == 64) ? ~0ull : ((1ull << n) - 1ull);
-    return s ? (((v << s) | (v >> (n - s))) & full) : v;
+// Packed position fields (m bits each, ascending, unused fields all ones) of the pattern
+// 2^kf (e + s): e shifted by s, then every position multiplied by 2^kf mod n.
+uint64_t pack_leader(uint64_t e, int s, int kf, int m, int n, int t) {
+    std::vector<int> pos;
+    for (int p = 0; p < n; ++p)
+        if ((e >> p) & 1ull) {
+            const int p1 = (p + s) % n;
+            pos.push_back(kf ? (((p1 << kf) | (p1 >> (m - kf))) & n) : p1);
+        }
+    std::sort(pos.begin(), pos.end());
+    uint64_t v = 0;
+    for (int f = t - 1; f >= 0; --f) v = (v << m) | (uint64_t)(f < (int)pos.size() ? pos[f] : n);
+    return v;
 }
 
-// Insert (key, mask) unless the key is present (then the mask must agree: the coset
+// Insert (key, positions) unless the key is present (then they must agree: the coset
 // leader is unique). Returns false on a disagreement (a logic error).
 bool tab_insert(HostTable &h, uint64_t key, uint64_t mask) {
     const uint32_t bm = (1u << h.bbits) - 1u;
@@ -238,7 +248,6 @@ int build_table(const Field &f, int t, HostTable &h) {
     h.t = t;
     TableDesc td{};
     const std::vector<uint8_t> blob = make_tables(f, t, &td);
-    const uint8_t *ex = blob.data() + td.off_exp;
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(blob.data() + td.off_log);
     std::vector<uint64_t> col(n, 0);  // packed odd-syndrome column of each position
     for (int p = 0; p < n; ++p)
@@ -248,15 +257,15 @@ int build_table(const Field &f, int t, HostTable &h) {
     // raw-region keys: every coprime syndrome zero (the key's region is the last one)
     int K = 0;
     for (int q = 0; q < t; ++q) K += f_coprime(q, n) ? 1 : 0;
-    // table size: <= 30 % of slots used (orbits ~ C(n, <=t) / n, plus raw-region keys)
+    // table size: <= ~50 % of slots used (orbits ~ C(n, <=t) / (n m), plus raw keys)
     double est = 0.0, c = 1.0;
     for (int w = 1; w <= t; ++w) {
         c = c * (n - w + 1) / w;
         est += c;
     }
-    est = est / n + 64;
+    est = est / ((double)n * m) * 1.05 + 64;
     h.bbits = 1;
-    while ((double)(kTabSlots << h.bbits) * 0.3 < est) ++h.bbits;
+    while ((double)(kTabSlots << h.bbits) * 0.5 < est) ++h.bbits;
     h.slots.assign((size_t(kTabSlots) << h.bbits) * 2, 0);
     // enumerate in parallel (threads own second positions), insert serially
     const int hw = (int)std::thread::hardware_concurrency();
@@ -264,10 +273,10 @@ int build_table(const Field &f, int t, HostTable &h) {
     std::vector<std::vector<uint64_t>> found(nth);  // (key, mask) pairs
     auto emit = [&](std::vector<uint64_t> &out, uint64_t S, uint64_t pat) {
         const uint32_t Sw[2] = {(uint32_t)S, (uint32_t)(S >> 32)};
-        const SyndKey k = keyf(Sw, t, lg, ex);
+        const SyndKey k = keyf(Sw, t, lg);
         if (((k.key - 1) >> 32) < (uint64_t)K) {  // a normalised region
             out.push_back(k.key);
-            out.push_back(rotl_mask(pat, k.s, n));  // the pattern shifted by +s
+            out.push_back(pack_leader(pat, k.s, k.kf, m, n, t));
             return;
         }
         for (int u = 0; u < n; ++u) {  // raw region: each shift is its own key
@@ -278,8 +287,9 @@ int build_table(const Field &f, int t, HostTable &h) {
                 Su |= uint64_t(w) << (8 * q);
             }
             const uint32_t Swu[2] = {(uint32_t)Su, (uint32_t)(Su >> 32)};
-            out.push_back(keyf(Swu, t, lg, ex).key);
-            out.push_back(rotl_mask(pat, u, n));
+            const SyndKey ku = keyf(Swu, t, lg);
+            out.push_back(ku.key);
+            out.push_back(pack_leader(pat, u + ku.s, ku.kf, m, n, t));  // ku.s == 0
         }
     };
     struct Rec {
@@ -358,13 +368,13 @@ struct bchk_ctx {
     FastFn fast = nullptr;
     bool use_fast = true;
     size_t lds_fast = 0, lds_coop = 0;
-    int grid_coop = 0;
+    int grid_coop = 0, grid_coop_tab = 0;
     uint32_t chunk_limit = 4;
     DevBuf queue, heavy, ctrl, diag;  // work queues + control words (one 128-B line each)
     uint8_t *d_tables = nullptr;
     hipStream_t stream = nullptr;
     size_t lds = 0, lds_alg = 0;
-    int grid = 0;
+    int grid = 0, grid_tab = 0;
     uint64_t max_decodes = 0;
     DevBuf y, res, l0, st, words, synd, ok;
     // the cooperative kernel runs on `aux`, concurrently with the exact kernel
@@ -482,6 +492,10 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     p.diag = (unsigned long long *)c->diag.p;
     p.diag_count = ctrl + kDiagCount;
 #endif
+    // kernel variant and its persistent grid: the syndrome-table kernels when the table is on
+    const bool tabk = p.tab.slots && c->ks.search_tab;
+    const int grid = tabk ? c->grid_tab : c->grid;
+    const int grid_coop = tabk ? c->grid_coop_tab : c->grid_coop;
     const bool conc = c->coop_concurrent && p.heavy_tail;
     hipStream_t cs = conc ? c->aux : s;  // the cooperative kernel's stream
     bchk_ctx::Ev ev{};
@@ -511,15 +525,15 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         q.qcount = ctrl;
         q.heads = ctrl + 32;
         // every resident wave may take work; waves beyond the queue length exit at once
-        HIP_TRY(launch_search(c->ks, q, c->grid, c->lds, s));
+        HIP_TRY(launch_search(c->ks, q, grid, c->lds, s));
     } else {
         const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
-        HIP_TRY(launch_search(c->ks, p, std::max(1, std::min(c->grid, need)), c->lds, s));
+        HIP_TRY(launch_search(c->ks, p, std::max(1, std::min(grid, need)), c->lds, s));
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[3], s));
     if (p.heavy_tail) {
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));
-        HIP_TRY(c->ks.coop(p, c->grid_coop, c->lds_coop, cs));
+        HIP_TRY(launch_coop(c->ks, p, grid_coop, c->lds_coop, cs));
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[5], cs));
     } else if (c->profile) {
         HIP_TRY(hipEventRecord(ev.e[4], s));
@@ -600,26 +614,22 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     int coop_target = 1;
     if (const char *cp = getenv("BCHK_COOP_PER_CU")) coop_target = std::max(1, atoi(cp));
     if (coop_target == 1) c->lds_coop = std::max<size_t>(c->lds_coop, 82 * 1024);
-    const void *cfn = c->ks.coop_ptr();
-    if (c->lds_coop > 65536)
-        (void)hipFuncSetAttribute(cfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_coop);
-    int coop_per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&coop_per_cu, cfn, kCoopThreads, c->lds_coop) != hipSuccess ||
-        coop_per_cu <= 0) {
-        coop_per_cu = 1;
-        (void)hipGetLastError();
+    // resident workgroups per CU of a kernel (its own registers; LDS as given)
+    auto grid_of = [&](const void *fn, int threads, size_t lds) {
+        if (lds > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess || per_cu <= 0) {
+            per_cu = 1;
+            (void)hipGetLastError();
+        }
+        return per_cu * prop.multiProcessorCount;
+    };
+    c->grid_coop = grid_of(c->ks.coop_ptr(), kCoopThreads, c->lds_coop);
+    c->grid = grid_of(c->ks.search_ptr(), kWaveSize * kWavesPerBlock, c->lds);
+    if (c->ks.search_tab) {
+        c->grid_coop_tab = grid_of(c->ks.coop_tab_ptr(), kCoopThreads, c->lds_coop);
+        c->grid_tab = grid_of(c->ks.search_tab_ptr(), kWaveSize * kWavesPerBlock, c->lds);
     }
-    c->grid_coop = coop_per_cu * prop.multiProcessorCount;
-    const void *fn = c->ks.search_ptr();
-    if (c->lds > 65536)
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveSize * kWavesPerBlock, c->lds) != hipSuccess ||
-        per_cu <= 0) {
-        per_cu = 1;
-        (void)hipGetLastError();
-    }
-    c->grid = per_cu * prop.multiProcessorCount;
     (void)rc;
     *out = c;
     return 0;
@@ -946,11 +956,11 @@ int bchk_syndrome_table_query(int m, int t, const uint32_t *synd, size_t N, uint
         uint64_t E = 0;
         bool hit = false;
         switch (m) {
-            case 2: hit = tab_decode<2, kTabTmax>(T, Sw, t, lg, ex, E); break;
-            case 3: hit = tab_decode<3, kTabTmax>(T, Sw, t, lg, ex, E); break;
-            case 4: hit = tab_decode<4, kTabTmax>(T, Sw, t, lg, ex, E); break;
-            case 5: hit = tab_decode<5, kTabTmax>(T, Sw, t, lg, ex, E); break;
-            default: hit = tab_decode<6, kTabTmax>(T, Sw, t, lg, ex, E); break;
+            case 2: hit = tab_decode<2, kTabTmax>(T, Sw, t, lg, E); break;
+            case 3: hit = tab_decode<3, kTabTmax>(T, Sw, t, lg, E); break;
+            case 4: hit = tab_decode<4, kTabTmax>(T, Sw, t, lg, E); break;
+            case 5: hit = tab_decode<5, kTabTmax>(T, Sw, t, lg, E); break;
+            default: hit = tab_decode<6, kTabTmax>(T, Sw, t, lg, E); break;
         }
         ok[i] = hit ? 1 : 0;
         if (err) err[i] = E;

@@ -26,6 +26,15 @@
 #include "bchk_core.h"
 #include "bchk_launch.h"
 
+// Tuning knobs (experiment builds override them): chunks per syndrome-table lookup group,
+// and calcL terms whose LDS loads are issued together.
+#ifndef BCHK_TAB_GROUP
+#define BCHK_TAB_GROUP 1
+#endif
+#ifndef BCHK_LSUM_BATCH
+#define BCHK_LSUM_BATCH 8
+#endif
+
 namespace bchk {
 
 // -------------------------------------------------------------- LDS layout
@@ -145,55 +154,97 @@ __device__ void prep_codeword(const SearchParams &p, const uint32_t *col, double
     }
 }
 
-// Decode test patterns i = base + lane (base a multiple of 64): returns success and
-// diff = yH ^ x (flipped pattern positions ^ error locations); for successful lanes also
-// m = calcM (:89-97) and l = calcL (:69-77), summed over diff in index order from the
-// wave's |alpha|-by-position LDS slice (lane-parallel; the ordered acceptance only
-// compares them).
-template <int M, int TMAX>
-__device__ __forceinline__ bool decode_chunk(const Prep<M, TMAX> &P, uint64_t base, int t,
-                                             const uint8_t *ex, const uint16_t *lg,
-                                             const uint64_t *chien, const double *ap,
-                                             const SyndTable &T,
-                                             Mask<Geo<M>::NW> &diff, int &m, double &l) {
+// Decode test patterns i = base + lane (base a multiple of 64) of G consecutive chunks
+// (bases base, base + 64, ...): success and diff = yH ^ x (flipped pattern positions ^
+// error locations); for successful lanes also m = calcM (:89-97) and l = calcL (:69-77),
+// summed over diff in index order from the wave's |alpha|-by-position LDS slice
+// (lane-parallel; the ordered acceptance only compares them). With the syndrome table the
+// G lookups are issued together, so a wave has G bucket loads in flight.
+template <int M, int TMAX, int G, bool TAB>
+__device__ __forceinline__ void decode_chunks(const Prep<M, TMAX> &P, uint64_t base, int t,
+                                              const uint8_t *ex, const uint16_t *lg,
+                                              const uint64_t *chien, const double *ap,
+                                              const SyndTable &T, Mask<Geo<M>::NW> (&diff)[G],
+                                              int (&m)[G], double (&l)[G], bool (&ok)[G]) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
     constexpr int NB = N < 31 ? N : 31;
-    uint32_t Sw[W];
-    Mask<NW> Pm = P.Plo;
+    uint32_t Sw[G][W];
+    Mask<NW> Pm[G], E[G];
 #pragma unroll
-    for (int w = 0; w < W; ++w) Sw[w] = P.S0[w] ^ P.Lo[w];
-    for (uint64_t hb = base >> 6; hb; hb &= hb - 1) {  // high pattern bits: wave-uniform
-        const int b = 6 + (int)__builtin_ctzll(hb);
-        if (b >= NB) continue;
-        const int pb = (int)rdl((uint32_t)P.ordb, b);
+    for (int g = 0; g < G; ++g) {
+        Pm[g] = P.Plo;
 #pragma unroll
-        for (int w = 0; w < W; ++w) Sw[w] ^= rdl(P.scol[w], b);
-        mask_set<NW>(Pm, pb);
-    }
-    Mask<NW> E;
-    bool ok;
-    if constexpr (M <= 6 && TMAX <= 8) {
-        if (T.slots) {
-            // the decoder as a table lookup (bchk_syndtab.h): identical result
-            ok = tab_decode<M, TMAX>(T, Sw, t, lg, ex, E.w[0]);
-        } else {
-            ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, t, E);
+        for (int w = 0; w < W; ++w) Sw[g][w] = P.S0[w] ^ P.Lo[w];
+        for (uint64_t hb = (base >> 6) + (uint64_t)g; hb; hb &= hb - 1) {  // wave-uniform
+            const int b = 6 + (int)__builtin_ctzll(hb);
+            if (b >= NB) continue;
+            const int pb = (int)rdl((uint32_t)P.ordb, b);
+#pragma unroll
+            for (int w = 0; w < W; ++w) Sw[g][w] ^= rdl(P.scol[w], b);
+            mask_set<NW>(Pm[g], pb);
         }
+    }
+    if constexpr (TAB) {
+        // the decoder as a table lookup (bchk_syndtab.h): identical result
+        SyndKey K[G];
+        uint32_t hb[G];
+        TabBucket B[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            K[g] = synd_key<M, TMAX>(Sw[g], t, lg);
+            hb[g] = tab_hash(K[g].key, T.bbits);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) tab_load(T, hb[g], B[g]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) ok[g] = tab_finish<M, TMAX>(T, K[g], hb[g], B[g], E[g].w[0]);
     } else {
-        ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, t, E);
+#pragma unroll
+        for (int g = 0; g < G; ++g) ok[g] = alg_decode_word<M, TMAX>(ex, lg, chien, Sw[g], t, E[g]);
     }
 #pragma unroll
-    for (int s = 0; s < NW; ++s) diff.w[s] = Pm.w[s] ^ E.w[s];
-    m = 0;
-    l = 0.0;
-    if (ok) {
-        m = mask_popc<NW>(diff);
+    for (int g = 0; g < G; ++g) {
 #pragma unroll
-        for (int s = 0; s < NW; ++s)
-            for (uint64_t v = diff.w[s]; v; v &= v - 1) l += ap[64 * s + (int)__builtin_ctzll(v)];
+        for (int s = 0; s < NW; ++s) diff[g].w[s] = Pm[g].w[s] ^ E[g].w[s];
+        m[g] = 0;
+        l[g] = 0.0;
+        if (ok[g]) {
+            m[g] = mask_popc<NW>(diff[g]);
+            if constexpr (NW == 1 && BCHK_LSUM_BATCH > 0) {
+                // calcL in index order (:69-77): the first KL terms' LDS loads are issued
+                // together, then summed in order (one LDS round trip instead of one per term)
+                constexpr int KL = BCHK_LSUM_BATCH > 0 ? BCHK_LSUM_BATCH : 1;
+                double v[KL];
+                uint64_t d = diff[g].w[0];
+#pragma unroll
+                for (int k = 0; k < KL; ++k) {
+                    v[k] = ap[d ? (int)__builtin_ctzll(d) : 0];
+                    d &= d - 1;
+                }
+                uint64_t e = diff[g].w[0];
+#pragma unroll
+                for (int k = 0; k < KL; ++k) {
+                    if (e) l[g] += v[k];
+                    e &= e - 1;
+                }
+                for (; d; d &= d - 1) l[g] += ap[(int)__builtin_ctzll(d)];
+            } else {
+#pragma unroll
+                for (int s = 0; s < NW; ++s)
+                    for (uint64_t v = diff[g].w[s]; v; v &= v - 1) l[g] += ap[64 * s + (int)__builtin_ctzll(v)];
+            }
+        }
     }
-    return ok;
 }
+
+// Chunks decoded per step (G). Measured on MI355X (profiles/r01_syndtab): G = 2 and 4
+// issue more lookups per wave but run slower (more registers, chunks published later), so
+// both kernels decode one chunk per step; the knob stays for experiment builds.
+template <bool TAB>
+constexpr int chunk_group() { return TAB ? BCHK_TAB_GROUP : 1; }
+// kernels with the table path exist for n <= 63 and t <= 8 (bchk_syndtab.h)
+template <int M, int TMAX>
+constexpr bool tab_capable() { return M <= 6 && TMAX <= 8; }
 
 // ----------------------------------------------------- sequential search state
 template <int NW>
@@ -333,7 +384,7 @@ __device__ void write_outputs(const SearchState<Geo<M>::NW> &S, const Prep<M, TM
 // ------------------------------------------------ wave-per-codeword search
 // 64 consecutive test patterns per step, acceptance in pattern order. A codeword still
 // running after p.chunk_limit steps is handed to the cooperative kernel (heavy queue).
-template <int M, int TMAX>
+template <int M, int TMAX, bool TAB>
 __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const uint16_t *lg,
                                 const uint32_t *col, const uint64_t *chien, double *as,
                                 double *ap, uint8_t *ordl, uint32_t cw, int lane) {
@@ -342,45 +393,65 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
     SearchState<NW> S;
     init_state<M>(S, p.variant);
+    constexpr int G = chunk_group<TAB>();
     uint32_t chunks = 0;
-    for (uint64_t base = 0;; base += 64, ++chunks) {
-        if (base >= S.bound) { S.i_end = S.bound; break; }
-        if (p.max_decodes && base >= p.max_decodes) { S.i_end = base; S.truncated = true; break; }
-        if (p.heavy_tail && chunks == p.chunk_limit) {
-            if (lane == 0) {  // longest-first: large remaining bounds to the front queue
-                uint32_t *slot = S.bound >= p.heavy_big
-                                     ? p.heavy_queue + atomicAdd(p.heavy_tail, 1u)
-                                     : p.heavy_queue + (p.count - 1u - atomicAdd(p.heavy_tail2, 1u));
-                __hip_atomic_store(slot, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            return;  // redone from scratch by kaneko_coop_kernel
-        }
-        Mask<NW> diff;
-        int m;
-        double l;
-        const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, p.tab, diff, m, l);
-        const uint64_t okm = ballot(ok);
-        if (base == 0 && !(okm & 1ull)) S.firstOK = false;  // :371
-        // Only improvements (l < l0) change the state: m0 at an improvement is the fixed
-        // i = 0 value or, once i = 0 has failed, the improving candidate's own m (:374), and
-        // l0 only decreases, so successes with l >= l0 can be skipped wholesale. The loop
-        // bound is NOT monotone (T comes from the calcT scan of each improvement, and
-        // (1 << T) - 1 wraps at 32 bits), so lanes are tested against the current bound.
-        uint64_t imp = ballot(ok && l < S.l0);
-        while (imp) {
-            const int L = (int)__builtin_ctzll(imp);
-            const uint64_t ii = base + (uint64_t)L;
-            if (ii >= S.bound) break;
-            const double lL = rdlf(l, L);
-            const int mL = (int)rdl((uint32_t)m, L);
-            Mask<NW> d;
+    for (uint64_t base0 = 0;; base0 += 64 * G) {
+        // the checks of the next chunk before any decode (no group started past the end)
+        if (base0 >= S.bound) { S.i_end = S.bound; break; }
+        if (p.max_decodes && base0 >= p.max_decodes) { S.i_end = base0; S.truncated = true; break; }
+        Mask<NW> diff[G];
+        int m[G];
+        double l[G];
+        bool ok[G];
+        bool handed = false;
+        if (!(p.heavy_tail && chunks >= p.chunk_limit))
+            decode_chunks<M, TMAX, G, TAB>(P, base0, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok);
 #pragma unroll
-            for (int s = 0; s < NW; ++s) d.w[s] = rdl64(diff.w[s], L);
-            accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
+        for (int g = 0; g < G; ++g) {
+            const uint64_t base = base0 + 64ull * (uint64_t)g;
+            if (base >= S.bound) { S.i_end = S.bound; S.done = true; break; }
+            if (p.max_decodes && base >= p.max_decodes) {
+                S.i_end = base;
+                S.truncated = true;
+                S.done = true;
+                break;
+            }
+            if (p.heavy_tail && chunks >= p.chunk_limit) {
+                if (lane == 0) {  // longest-first: large remaining bounds to the front queue
+                    uint32_t *slot = S.bound >= p.heavy_big
+                                         ? p.heavy_queue + atomicAdd(p.heavy_tail, 1u)
+                                         : p.heavy_queue + (p.count - 1u - atomicAdd(p.heavy_tail2, 1u));
+                    __hip_atomic_store(slot, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                handed = true;  // redone from scratch by kaneko_coop_kernel
+                break;
+            }
+            ++chunks;
+            const uint64_t okm = ballot(ok[g]);
+            if (base == 0 && !(okm & 1ull)) S.firstOK = false;  // :371
+            // Only improvements (l < l0) change the state: m0 at an improvement is the fixed
+            // i = 0 value or, once i = 0 has failed, the improving candidate's own m (:374),
+            // and l0 only decreases, so successes with l >= l0 can be skipped wholesale. The
+            // loop bound is NOT monotone (T comes from the calcT scan of each improvement,
+            // and (1 << T) - 1 wraps at 32 bits), so lanes meet the current bound.
+            uint64_t imp = ballot(ok[g] && l[g] < S.l0);
+            while (imp) {
+                const int L = (int)__builtin_ctzll(imp);
+                const uint64_t ii = base + (uint64_t)L;
+                if (ii >= S.bound) break;
+                const double lL = rdlf(l[g], L);
+                const int mL = (int)rdl((uint32_t)m[g], L);
+                Mask<NW> d;
+#pragma unroll
+                for (int s = 0; s < NW; ++s) d.w[s] = rdl64(diff[g].w[s], L);
+                accept_success<M, TMAX>(S, P, d, mL, lL, ii, as, p, lane);
+                if (S.done) break;
+                // l0 dropped: re-filter the later lanes of this chunk
+                imp = ballot(ok[g] && l[g] < S.l0) & ~((2ull << L) - 1ull);
+            }
             if (S.done) break;
-            // l0 dropped: re-filter the later lanes of this chunk
-            imp = ballot(ok && l < S.l0) & ~((2ull << L) - 1ull);
         }
+        if (handed) return;
         if (S.done) break;
     }
     write_outputs<M, TMAX>(S, P, p, cw, lane);
@@ -408,7 +479,7 @@ __device__ __forceinline__ void wave_done(const SearchParams &p, int lane, uint3
     }
 }
 
-template <int M, int TMAX>
+template <int M, int TMAX, bool TAB>
 __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock)
 kaneko_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -428,7 +499,7 @@ kaneko_search_kernel(SearchParams p) {
         const uint32_t stride = gridDim.x * kWavesPerBlock;
         uint32_t ndone = 0;
         for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride, ++ndone)
-            search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ap, ordl, cw, lane);
+            search_codeword<M, TMAX, TAB>(p, ex, lg, col, chien, as, ap, ordl, cw, lane);
         wave_done(p, lane, ndone);
         return;
     }
@@ -448,7 +519,7 @@ kaneko_search_kernel(SearchParams p) {
             ++exhausted;
             continue;
         }
-        search_codeword<M, TMAX>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane);
+        search_codeword<M, TMAX, TAB>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane);
         ++ndone;
     }
     wave_done(p, lane, ndone);
@@ -463,7 +534,17 @@ kaneko_search_kernel(SearchParams p) {
 // acceptance (:361-405) to the candidates, and publishes the loop bound and l0 that the
 // decoders read to stop early and filter candidates. No workgroup barrier per chunk.
 // Results are identical to the single-wave search.
-constexpr int kCoopSlots = 16;
+// Ring slots: chunks in flight between the decoders and the acceptor. With 15 decoder
+// waves each holding G chunks while a table lookup is outstanding, the ring -- not the
+// decoders -- bounds the rate (chunks in flight / chunk latency): n <= 63 gets a deep ring
+// (1.3 KB per slot), longer codes keep 16.
+#ifndef BCHK_COOP_SLOTS
+#define BCHK_COOP_SLOTS 48
+#endif
+constexpr int kCoopSlotsMax = 64;
+template <int NW>
+constexpr int coop_slots() { return NW == 1 ? BCHK_COOP_SLOTS : 16; }
+static_assert(BCHK_COOP_SLOTS <= kCoopSlotsMax, "ring flags are polled one slot per lane");
 constexpr uint32_t kSpinLimit = 1u << 24;  // ~1 s of polling: a guard against logic errors
 
 template <int NW>
@@ -482,7 +563,7 @@ struct CoopCtl {
     uint32_t drec;      // diagnostic builds: its record index
     uint64_t bound;     // the acceptor's current loop bound (diagnostics; may rise again)
     double l0;          // current l0 (monotone non-increasing)
-    uint32_t ready[kCoopSlots];  // chunk index + 1 once the slot holds that chunk
+    uint32_t ready[kCoopSlotsMax];  // chunk index + 1 once the slot holds that chunk
 };
 
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t *a) {
@@ -541,12 +622,13 @@ __device__ uint32_t next_heavy(const SearchParams &p) {
     return kEmptySlot;
 }
 
-template <int M, int TMAX>
+template <int M, int TMAX, bool TAB>
 __global__ void __launch_bounds__(kWaveSize * kCoopWaves)
 kaneko_coop_kernel(SearchParams p) {
     constexpr int NW = Geo<M>::NW;
     constexpr int NP = Smem<M, TMAX>::NP;
     constexpr int kAcceptor = 0;  // the oldest wave: the SIMD arbiter favours it
+    constexpr int kCoopSlots = coop_slots<NW>();
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
     const uint8_t *ex = smem + p.td.off_exp;
@@ -602,59 +684,66 @@ kaneko_coop_kernel(SearchParams p) {
 #endif
         if (wid != kAcceptor) {
             // ------------------------------------------------------------ decoder
+            constexpr int G = chunk_group<TAB>();
             for (;;) {
-                uint32_t c = 0;
-                if (lane == 0) c = atomicAdd(&ctl->next, 1u);
+                uint32_t c = 0;  // this wave decodes chunks c .. c + G - 1
+                if (lane == 0) c = atomicAdd(&ctl->next, (uint32_t)G);
                 c = (uint32_t)__shfl((int)c, 0, 64);
                 const uint64_t base = 64ull * c;
                 // no early stop on the published loop bound: it can rise again after a later
                 // improvement (T is not monotone), so only the acceptor decides the end; the
                 // ring keeps decoders at most kCoopSlots chunks ahead of it
                 if (base >= capc || lds_ld(&ctl->done)) break;
-                // the slot is free once the acceptor has finished chunk c - kCoopSlots
+                // the slots are free once the acceptor has finished chunk c + G - 1 - kCoopSlots
                 bool stop = false;
-                for (uint32_t spins = 0; c >= lds_ld(&ctl->consumed) + kCoopSlots; ++spins) {
+                for (uint32_t spins = 0; c + (uint32_t)(G - 1) >= lds_ld(&ctl->consumed) + kCoopSlots; ++spins) {
                     if (lds_ld(&ctl->done) || spins > kSpinLimit) { stop = true; break; }
                     __builtin_amdgcn_s_sleep(2);
                 }
                 if (stop) break;
                 const double l0r = __longlong_as_double((long long)lds_ld64(
                     reinterpret_cast<const uint64_t *>(&ctl->l0)));
-                Mask<NW> diff;
-                int m;
-                double l;
-                const bool ok = decode_chunk<M, TMAX>(P, base, p.t, ex, lg, chien, ap, p.tab, diff, m, l);
-                const uint64_t okm = ballot(ok);
-                // candidates: the strict running minima of l over this chunk's successes,
-                // below l0 as last published. The improvements are the running minima over
-                // all successes in pattern order, so they are a subset of these.
-                const uint64_t cm = ballot(ok && l < l0r);
-                uint64_t cand = 0;
-                double run = l0r;
-                for (uint64_t mm = cm; mm; mm &= mm - 1) {
-                    const int L = (int)__builtin_ctzll(mm);
-                    const double lv = rdlf(l, L);
-                    if (lv < run) {
-                        cand |= 1ull << L;
-                        run = lv;
-                    }
-                }
-                CoopSlot<NW> &sl = ring[c % kCoopSlots];
-                if ((cand >> lane) & 1ull) {
+                Mask<NW> diff[G];
+                int m[G];
+                double l[G];
+                bool ok[G];
+                decode_chunks<M, TMAX, G, TAB>(P, base, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok);
 #pragma unroll
-                    for (int s2 = 0; s2 < NW; ++s2) sl.diff[lane * NW + s2] = diff.w[s2];
-                    sl.m[lane] = (uint32_t)m;
-                    sl.l[lane] = l;
-                }
-                if (lane == 0) {
-                    sl.okm = okm;
-                    sl.cand = cand;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0) lds_st(&ctl->ready[c % kCoopSlots], c + 1u);
+                for (int g = 0; g < G; ++g) {
+                    const uint32_t cg = c + (uint32_t)g;
+                    if (64ull * cg >= capc) break;  // past the cap: never read by the acceptor
+                    const uint64_t okm = ballot(ok[g]);
+                    // candidates: the strict running minima of l over this chunk's successes,
+                    // below l0 as last published. The improvements are the running minima
+                    // over all successes in pattern order, so they are a subset of these.
+                    const uint64_t cm = ballot(ok[g] && l[g] < l0r);
+                    uint64_t cand = 0;
+                    double run = l0r;
+                    for (uint64_t mm = cm; mm; mm &= mm - 1) {
+                        const int L = (int)__builtin_ctzll(mm);
+                        const double lv = rdlf(l[g], L);
+                        if (lv < run) {
+                            cand |= 1ull << L;
+                            run = lv;
+                        }
+                    }
+                    CoopSlot<NW> &sl = ring[cg % kCoopSlots];
+                    if ((cand >> lane) & 1ull) {
+#pragma unroll
+                        for (int s2 = 0; s2 < NW; ++s2) sl.diff[lane * NW + s2] = diff[g].w[s2];
+                        sl.m[lane] = (uint32_t)m[g];
+                        sl.l[lane] = l[g];
+                    }
+                    if (lane == 0) {
+                        sl.okm = okm;
+                        sl.cand = cand;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) lds_st(&ctl->ready[cg % kCoopSlots], cg + 1u);
 #ifdef BCHK_DIAG
-                dg[3] += 1;
+                    dg[3] += 1;
 #endif
+                }
             }
         } else {
             // ------------------------------------------------------------ acceptor
@@ -858,15 +947,15 @@ __global__ void __launch_bounds__(256) count_kernel(const uint8_t *tx, const uin
 }
 
 // ------------------------------------------------------------- launchers
-template <int M, int TMAX>
+template <int M, int TMAX, bool TAB>
 static hipError_t launch_search_impl(const SearchParams &p, int grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((kaneko_search_kernel<M, TMAX>), dim3(grid), dim3(kWaveSize * kWavesPerBlock),
-                       lds, s, p);
+    hipLaunchKernelGGL((kaneko_search_kernel<M, TMAX, TAB>), dim3(grid),
+                       dim3(kWaveSize * kWavesPerBlock), lds, s, p);
     return hipGetLastError();
 }
-template <int M, int TMAX>
+template <int M, int TMAX, bool TAB>
 static hipError_t launch_coop_impl(const SearchParams &p, int grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((kaneko_coop_kernel<M, TMAX>), dim3(grid), dim3(kWaveSize * kCoopWaves),
+    hipLaunchKernelGGL((kaneko_coop_kernel<M, TMAX, TAB>), dim3(grid), dim3(kWaveSize * kCoopWaves),
                        lds, s, p);
     return hipGetLastError();
 }
@@ -876,19 +965,32 @@ static hipError_t launch_alg_impl(const AlgParams &p, size_t lds, hipStream_t s)
     hipLaunchKernelGGL((alg_decode_kernel<M, TMAX>), dim3(grid), dim3(256), lds, s, p);
     return hipGetLastError();
 }
-template <int M, int TMAX>
-static const void *search_fn() { return reinterpret_cast<const void *>(&kaneko_search_kernel<M, TMAX>); }
-template <int M, int TMAX>
-static const void *coop_fn() { return reinterpret_cast<const void *>(&kaneko_coop_kernel<M, TMAX>); }
+template <int M, int TMAX, bool TAB>
+static const void *search_fn() { return reinterpret_cast<const void *>(&kaneko_search_kernel<M, TMAX, TAB>); }
+template <int M, int TMAX, bool TAB>
+static const void *coop_fn() { return reinterpret_cast<const void *>(&kaneko_coop_kernel<M, TMAX, TAB>); }
 
 template <int M, int TMAX>
 static KernelSet make_set() {
     constexpr int NW = Geo<M>::NW;
-    const size_t coop = sizeof(CoopSlot<NW>) * kCoopSlots + sizeof(CoopCtl) +
+    const size_t coop = sizeof(CoopSlot<NW>) * coop_slots<NW>() + sizeof(CoopCtl) +
                         (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES;
-    return KernelSet{&launch_search_impl<M, TMAX>, &launch_coop_impl<M, TMAX>, &coop_fn<M, TMAX>, coop,
-                     &launch_alg_impl<M, TMAX>, &search_fn<M, TMAX>, TMAX,
-                     (size_t)Smem<M, TMAX>::WAVE_BYTES};
+    KernelSet k{};
+    k.search = &launch_search_impl<M, TMAX, false>;
+    k.coop = &launch_coop_impl<M, TMAX, false>;
+    k.coop_ptr = &coop_fn<M, TMAX, false>;
+    k.search_ptr = &search_fn<M, TMAX, false>;
+    if constexpr (tab_capable<M, TMAX>()) {
+        k.search_tab = &launch_search_impl<M, TMAX, true>;
+        k.coop_tab = &launch_coop_impl<M, TMAX, true>;
+        k.coop_tab_ptr = &coop_fn<M, TMAX, true>;
+        k.search_tab_ptr = &search_fn<M, TMAX, true>;
+    }
+    k.coop_bytes = coop;
+    k.alg = &launch_alg_impl<M, TMAX>;
+    k.tmax = TMAX;
+    k.wave_bytes = (size_t)Smem<M, TMAX>::WAVE_BYTES;
+    return k;
 }
 
 // TMAX buckets: smallest instantiated bucket >= t.
@@ -907,7 +1009,10 @@ bool select_kernels(int m, int t, KernelSet *out) {
 }
 
 hipError_t launch_search(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s) {
-    return k.search(p, grid, lds, s);
+    return (p.tab.slots && k.search_tab) ? k.search_tab(p, grid, lds, s) : k.search(p, grid, lds, s);
+}
+hipError_t launch_coop(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s) {
+    return (p.tab.slots && k.coop_tab) ? k.coop_tab(p, grid, lds, s) : k.coop(p, grid, lds, s);
 }
 hipError_t launch_alg(const KernelSet &k, const AlgParams &p, size_t lds, hipStream_t s) {
     return k.alg(p, lds, s);

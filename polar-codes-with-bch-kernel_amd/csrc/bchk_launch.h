@@ -6,13 +6,19 @@
 
 namespace bchk {
 
+// Kernel entry points of one (m, TMAX) instantiation. The *_tab variants decode test
+// patterns through the syndrome table (bchk_syndtab.h); null where (m, TMAX) has none.
 struct KernelSet {
     hipError_t (*search)(const SearchParams &, int, size_t, hipStream_t);
     hipError_t (*coop)(const SearchParams &, int, size_t, hipStream_t);
     const void *(*coop_ptr)();
+    const void *(*search_ptr)();
+    hipError_t (*search_tab)(const SearchParams &, int, size_t, hipStream_t);
+    hipError_t (*coop_tab)(const SearchParams &, int, size_t, hipStream_t);
+    const void *(*coop_tab_ptr)();
+    const void *(*search_tab_ptr)();
     size_t coop_bytes;  // LDS bytes of the cooperative kernel beyond the tables
     hipError_t (*alg)(const AlgParams &, size_t, hipStream_t);
-    const void *(*search_ptr)();
     int tmax;
     size_t wave_bytes;  // LDS bytes per wave of the search kernel
 };
@@ -26,7 +32,9 @@ int fast_block_waves();  // waves per block of the fast kernel
 
 // Picks the (m, TMAX) instantiation for runtime t (smallest TMAX >= t).
 bool select_kernels(int m, int t, KernelSet *out);
+// search / cooperative kernel: the table variant when p.tab.slots is set and it exists
 hipError_t launch_search(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s);
+hipError_t launch_coop(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s);
 constexpr int kCoopThreads = 1024;
 hipError_t launch_alg(const KernelSet &k, const AlgParams &p, size_t lds, hipStream_t s);
 hipError_t launch_count(int n, const uint8_t *tx, const uint8_t *res, const bchk_stats *st,

@@ -16,11 +16,13 @@
 // (= 1) and the zero syndromes before it leave the key. The key is (region k = ordinal of
 // q*, packed remaining syndromes); syndromes whose coprime entries are all zero form the
 // last region, keyed by the raw remaining syndromes (s = 0). The table stores, per key,
-// the error mask of the normalised pattern; the caller rotates it back by s. For
-// BCH(63,30,13) that is ~1.2 M keys (one per shift orbit of the 75.6 M patterns), held in
-// an open-addressed table of 64-B buckets (4 slots of {key, mask}), 64 MiB: one bucket
-// load per lookup in the common case, resident in the 256 MB Infinity Cache while the
-// search kernels run. Built once per (m, t) on the host, uploaded once per device.
+// positions of the normalised pattern; the caller maps them back. For BCH(63,30,13) that is
+// ~1.2 M shift orbits of the 75.6 M patterns, held in
+// an open-addressed table of 64-B buckets (4 slots of {key, positions}). Squaring all
+// syndromes (the Frobenius map: positions times 2 mod n) also preserves correctability,
+// so keys are canonical over that orbit too: ~0.2 M keys, 8 MiB, one bucket load per
+// lookup in the common case, mostly L2 / Infinity-Cache resident while the search kernels
+// run. Built once per (m, t) on the host, uploaded once per device.
 //
 // tests/test_filter.py checks every lookup against the oracle's Decoder::decode (the small
 // codes exhaustively); tests/test_gpu_parity.py runs every path with and without it.
@@ -72,16 +74,30 @@ struct TabConsts {
 };
 
 struct SyndKey {
-    uint64_t key;  // (region << 32 | packed syndromes) + 1, never 0
+    uint64_t key;  // (region << 32 | canonical packed log-syndromes) + 1, never 0
     int s;         // normalising shift
+    int kf;        // Frobenius power of the canonical form
+    int t;         // position fields in a table entry
 };
 
-// Normalised key of packed odd syndromes Sw (byte q of word q/4 is S_(2q+1)), runtime
-// t <= TMAX. lg: log table with lg[0] = 2n - 1; ex: exp table over [0, 2n) with
-// ex[2n - 1] = 0 (bchk_device.h TableDesc). Branch-free; identical on host and device.
+// rotate an m-bit field left by k in [0, m) (= multiply by 2^k mod n for values < n; the
+// all-ones value n, used as "zero element" / "no position", is fixed)
+template <int M>
+__host__ __device__ __forceinline__ int rotl_m(int v, int k) {
+    constexpr int N = (1 << M) - 1;
+    return ((v << k) | (v >> (M - k))) & N;
+}
+
+// Canonical key of packed odd syndromes Sw (byte q of word q/4 is S_(2q+1)), runtime
+// t <= TMAX. lg: log table with lg[0] = 2n - 1 (bchk_device.h TableDesc). The key packs,
+// for every odd index left in it, the log of the normalised syndrome (n for a zero one),
+// m bits each. Squaring every syndrome (the Frobenius map, = the pattern's positions times
+// 2 mod n) rotates each field left by one bit, so the least of the m rotations is a key
+// shared by the whole (shift x Frobenius) orbit; kf records which rotation it was.
+// Branch-free; identical on host and device.
 template <int M, int TMAX>
 __host__ __device__ __forceinline__ SyndKey synd_key(const uint32_t *Sw, int t,
-                                                     const uint16_t *lg, const uint8_t *ex) {
+                                                     const uint16_t *lg) {
     constexpr int N = (1 << M) - 1;
     constexpr TabConsts<N, TMAX> C{};
     uint32_t S[TMAX];
@@ -103,26 +119,40 @@ __host__ __device__ __forceinline__ SyndKey synd_key(const uint32_t *Sw, int t,
         k += (!nz && !found && q < t) ? 1 : 0;
         found = found || nz;
     }
-    // remaining syndromes times alpha^(j s): the exponent ls + (j s mod n) is < 2n - 1
-    // when S_j != 0 and >= 2n - 1 (clamped to the zero entry) when S_j = 0
+    // log of alpha^(j s) S_j = ls + (j s mod n), reduced mod n; n marks S_j = 0
     const int d2 = (2 * s >= N) ? 2 * s - N : 2 * s;  // 2 s mod n
     int r = s;                                         // j s mod n for j = 1, 3, 5, ...
     uint64_t idx = 0;
     int ord = 0;
+    uint64_t lo = 0;  // bit 0 of every field: the SWAR field-rotation masks
 #pragma unroll
     for (int q = 0; q < TMAX; ++q) {
         const bool incl = q < t && (!C.cop[q] || ord > k);
         ord += C.cop[q] ? 1 : 0;
         int e = ls[q] + r;
-        e = e < 2 * N - 1 ? e : 2 * N - 1;
-        const uint64_t v = ex[e];
-        idx = incl ? ((idx << M) | v) : idx;
+        e = e >= N ? e - N : e;
+        e = S[q] ? e : N;
+        idx = incl ? ((idx << M) | (uint64_t)e) : idx;
+        lo = incl ? ((lo << M) | 1ull) : lo;
         r += d2;
         r = r >= N ? r - N : r;
     }
+    // least rotation over the m Frobenius conjugates (each field rotated by the same k)
+    const uint64_t top = lo << (M - 1);       // bit m-1 of every field
+    const uint64_t full = lo * (uint64_t)N;   // every field bit
+    uint64_t best = idx, cur = idx;
+    int kf = 0;
+#pragma unroll
+    for (int f = 1; f < M; ++f) {
+        cur = (((cur << 1) & ~lo) | ((cur & top) >> (M - 1))) & full;
+        kf = cur < best ? f : kf;
+        best = cur < best ? cur : best;
+    }
     SyndKey out;
-    out.key = (((uint64_t)k << 32) | idx) + 1ull;
+    out.key = (((uint64_t)k << 32) | best) + 1ull;
     out.s = s;
+    out.kf = kf;
+    out.t = t;
     return out;
 }
 
@@ -130,41 +160,79 @@ __host__ __device__ __forceinline__ uint32_t tab_hash(uint64_t key, uint32_t bbi
     return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - bbits));
 }
 
-// rotate an n-bit mask (n <= 63) right by s in [0, n): position p -> p - s (mod n)
-template <int N>
-__host__ __device__ __forceinline__ uint64_t rotr_n(uint64_t v, int s) {
-    constexpr uint64_t FULL = (1ull << N) - 1ull;
-    return s ? (((v >> s) | (v << (N - s))) & FULL) : v;
+// Stored pattern: t position fields of m bits (unused fields all ones) of the canonical
+// syndrome's leader P = 2^kf (e + s). Back to e: p = 2^-kf p' - s (mod n) per field.
+template <int M, int TMAX>
+__host__ __device__ __forceinline__ uint64_t tab_unmap(uint64_t packed, int s, int kf, int t) {
+    constexpr int N = (1 << M) - 1;
+    uint64_t E = 0;
+#pragma unroll
+    for (int f = 0; f < TMAX; ++f) {
+        const int pp = f < t ? (int)((packed >> (M * f)) & (uint64_t)N) : N;
+        int p = rotl_m<M>(pp, kf ? M - kf : 0) - s;
+        p = p < 0 ? p + N : p;
+        E |= (pp != N) ? (1ull << p) : 0ull;
+    }
+    return E;
+}
+
+// One 64-B bucket: kTabSlots {key, packed positions}.
+struct TabBucket {
+    uint64_t k[kTabSlots], v[kTabSlots];
+};
+
+__host__ __device__ __forceinline__ void tab_load(const SyndTable &T, uint32_t b, TabBucket &B) {
+    const uint64_t *bk = T.slots + (size_t)b * (2 * kTabSlots);
+#pragma unroll
+    for (int j = 0; j < kTabSlots; ++j) {
+        B.k[j] = bk[2 * j];
+        B.v[j] = bk[2 * j + 1];
+    }
+}
+
+// Finish a lookup from its home bucket (already loaded): further buckets only when the
+// home bucket is full without the key (linear probing; no key sits more than
+// T.max_probe - 1 buckets past its home).
+template <int M, int TMAX>
+__host__ __device__ __forceinline__ bool tab_finish(const SyndTable &T, const SyndKey &K,
+                                                    uint32_t b, const TabBucket &B0, uint64_t &E) {
+    uint64_t v = 0;
+    bool hit = false, open = false;
+#pragma unroll
+    for (int j = 0; j < kTabSlots; ++j) {
+        v = (B0.k[j] == K.key) ? B0.v[j] : v;
+        hit = hit || B0.k[j] == K.key;
+        open = open || B0.k[j] == 0ull;
+    }
+    if (!hit && !open) {
+        const uint32_t bm = (1u << T.bbits) - 1u;
+        for (uint32_t p = 1; p < T.max_probe; ++p) {
+            b = (b + 1u) & bm;
+            TabBucket B;
+            tab_load(T, b, B);
+#pragma unroll
+            for (int j = 0; j < kTabSlots; ++j) {
+                v = (B.k[j] == K.key) ? B.v[j] : v;
+                hit = hit || B.k[j] == K.key;
+                open = open || B.k[j] == 0ull;
+            }
+            if (hit || open) break;
+        }
+    }
+    E = hit ? tab_unmap<M, TMAX>(v, K.s, K.kf, K.t) : 0ull;
+    return hit;
 }
 
 // Decoder::decode of one test word from its odd syndromes, by table lookup: true and E =
-// the flipped positions iff the syndrome is correctable. Probes at most T.max_probe
-// buckets (linear probing: no key sits further from its home bucket).
+// the flipped positions iff the syndrome is correctable.
 template <int M, int TMAX>
 __host__ __device__ __forceinline__ bool tab_decode(const SyndTable &T, const uint32_t *Sw, int t,
-                                                    const uint16_t *lg, const uint8_t *ex,
-                                                    uint64_t &E) {
-    constexpr int N = (1 << M) - 1;
-    const SyndKey K = synd_key<M, TMAX>(Sw, t, lg, ex);
-    const uint32_t bm = (1u << T.bbits) - 1u;
-    uint32_t b = tab_hash(K.key, T.bbits);
-    uint64_t mask = 0;
-    bool hit = false;
-    for (uint32_t p = 0; p < T.max_probe; ++p) {
-        const uint64_t *bk = T.slots + (size_t)b * (2 * kTabSlots);
-        bool open = false;
-#pragma unroll
-        for (int j = 0; j < kTabSlots; ++j) {
-            const uint64_t k = bk[2 * j], v = bk[2 * j + 1];
-            mask = (k == K.key) ? v : mask;
-            hit = hit || k == K.key;
-            open = open || k == 0ull;
-        }
-        if (hit || open) break;
-        b = (b + 1u) & bm;
-    }
-    E = hit ? rotr_n<N>(mask, K.s) : 0ull;
-    return hit;
+                                                    const uint16_t *lg, uint64_t &E) {
+    const SyndKey K = synd_key<M, TMAX>(Sw, t, lg);
+    const uint32_t b = tab_hash(K.key, T.bbits);
+    TabBucket B;
+    tab_load(T, b, B);
+    return tab_finish<M, TMAX>(T, K, b, B, E);
 }
 
 }  // namespace bchk

@@ -84,9 +84,10 @@ def test_table_matches_decoder(m, t, count):
 
 def test_table_size_and_probes():
     keys, nbytes, probe = load().syndrome_table_info(6, 6)
-    # one key per shift orbit of the 75.6 M weight <= 6 patterns of length 63 (+ raw keys)
-    assert 1_190_000 < keys < 1_300_000
-    assert nbytes <= 64 << 20 and 1 <= probe <= 16
+    # one key per (cyclic shift x Frobenius) orbit of the 75.6 M weight <= 6 patterns of
+    # length 63: ~75.6 M / (63 * 6), plus orbits smaller than 378 and raw-region keys
+    assert 195_000 < keys < 215_000
+    assert nbytes <= 16 << 20 and 1 <= probe <= 16
 
 
 def test_table_rejects_infeasible():
