@@ -210,12 +210,15 @@ def main():
         k["GB_s"] = (bytes_per_cw * k["codewords"] / (k["ms"] / 1e3) / 1e9) if k["ms"] > 0 else 0.0
     dom = max(kern, key=lambda k: k["ms"])
     achieved = dom["GB_s"]
+    # HBM bytes per launch of the dominant kernel, from the committed PMC passes of the same
+    # workload (scripts/gpu_final.sh -> scripts/traffic_json.py): FETCH_SIZE x 2 (gfx950)
+    # + WRITE_SIZE, null when no profile of this workload exists
     traffic = None
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
             if tr.get("batch") == B and tr.get("snr_db") == args.snr and tr.get("J") == args.J:
-                traffic = tr.get("hbm_bytes_per_launch")
+                traffic = tr.get("kernels", {}).get(dom["name"].replace(" ", ""))
         except Exception:
             traffic = None
     if rank == 0:
