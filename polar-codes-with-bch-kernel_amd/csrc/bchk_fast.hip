@@ -10,8 +10,8 @@
 //     them with a 64-key bitonic network in registers;
 //   - distinct prefixes order alpha = |2y/s2| exactly; a prefix tie within the sorted
 //     prefix calcRightSide can touch (2t+1 entries) sends the codeword to the exact slow
-//     path; the alphas that enter sums are recomputed exactly (IEEE f64 division of the
-//     row's samples, gathered on demand);
+//     path; calcL sums exact alphas (IEEE f64 division of the samples at the flipped
+//     positions, gathered on demand); calcRightSide is bounded below from the keys alone;
 //   - decodes i = 0 and i = 1 run per lane (binary BM + Chien table);
 //   - calcL / calcRightSide are summed in the reference's order.
 // Codewords not resolved here (no early return at i <= 1, or any doubt) are appended to a
@@ -185,8 +185,13 @@ kaneko_fast_kernel(SearchParams p) {
         bad = b != 0u;
     }
 
-    // ---- the sorted prefix calcRightSide can touch: positions packed 5 per word, their
-    // alphas computed once (IEEE f64 division, as the reference) from one batch of loads
+    // ---- the sorted prefix calcRightSide can touch: positions packed 5 per word, and a
+    // lower bound of each alpha from its key alone: the prefix is |y| truncated to 21
+    // mantissa bits, so ylo <= |y| < ylo (1 + 2^-20), and lo = ylo * RN(2/s2) lies below
+    // alpha = RN(2|y|/s2) by at most a relative 2^-51. The row is not re-read: the fast
+    // path returns only when l < (sum of lo) (1 - 2^-40) <= calcRightSide(), and queues
+    // every other case (a relative window of 2^-19 more than the exact test) for the
+    // exact kernel.
     constexpr int NPF = KMAX + 1;
     constexpr int NPW = (NPF + 4) / 5;
     uint32_t ppk[NPW];
@@ -196,13 +201,16 @@ kaneko_fast_kernel(SearchParams p) {
     for (int r = 0; r < NPF; ++r) ppk[r / 5] |= (key[r] & 63u) << (6 * (r % 5));
     auto ppos = [&](int r) { return (int)((ppk[r / 5] >> (6 * (r % 5))) & 63u); };
     const int o0 = (int)(key[0] & 63u);
-    double apf[NPF];
+    double alo[NPF];
     {
-        double yv[NPF];
+        const double c2 = 2.0 / s2;
 #pragma unroll
-        for (int r = 0; r < NPF; ++r) yv[r] = yrow[ppos(r)];
-#pragma unroll
-        for (int r = 0; r < NPF; ++r) apf[r] = fabs((2.0 * yv[r]) / s2);
+        for (int r = 0; r < NPF; ++r) {
+            const uint32_t pre = key[r] >> 6;  // eb (5 bits) | 21 mantissa bits
+            const uint64_t bits = ((uint64_t)((pre >> 21) + (1023u - 27u)) << 52) |
+                                  ((uint64_t)(pre & 0x1FFFFFu) << 31);
+            alo[r] = __longlong_as_double((long long)bits) * c2;
+        }
     }
     // ---- syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
     uint32_t S0[W];
@@ -217,7 +225,7 @@ kaneko_fast_kernel(SearchParams p) {
 
     BCHK_STAMP(2)
 #if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 3
-    if (p.l0 && live) p.l0[cw] = (double)(apf[0] + apf[NPF - 1] + (double)(S0[0] ^ ppk[0] ^ (uint32_t)bad));
+    if (p.l0 && live) p.l0[cw] = (double)(alo[0] + alo[NPF - 1] + (double)(S0[0] ^ ppk[0] ^ (uint32_t)bad));
     return;
 #endif
     // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`
@@ -240,17 +248,18 @@ kaneko_fast_kernel(SearchParams p) {
             if (v) l += fabs((2.0 * g[j]) / s2);
             v &= v - 1;
         }
-        double rs = 0.0;
+        double rs_lo = 0.0;  // lower bound of calcRightSide() (:54-67)
         int taken = 0;
 #pragma unroll
         for (int r = 0; r < NPF; ++r) {
             const bool ag = !((diff >> ppos(r)) & 1ull);
             if (ag && taken < border) {
-                rs += apf[r];
+                rs_lo += alo[r];
                 ++taken;
             }
         }
-        ret = (taken >= border) && (l < rs);  // otherwise: ran past the exact prefix / no return
+        // a certain return only: l < rs_lo (1 - 2^-40) <= rs; the exact path decides the rest
+        ret = (taken >= border) && (l < rs_lo * (1.0 - 0x1p-40));
     };
 
     // ---- i = 0 (:361-382)
