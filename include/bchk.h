@@ -153,6 +153,34 @@ int bchk_syndrome_table_query(int m, int t, const uint32_t *synd, size_t N, uint
 /* Size of that table: distinct keys, bytes, longest probe sequence (buckets). */
 int bchk_syndrome_table_info(int m, int t, uint64_t *keys, uint64_t *bytes, uint32_t *max_probe);
 
+/* ---- SC-list decoding of polar codes (the reference's vendored library, never built by
+ * the reference itself: headers/external/MixedKernelListDecoder.h:10-42). */
+typedef struct bchk_polar bchk_polar;
+/* Replaces CMixedKernelListDecoder(std::istream& Spec, unsigned ListSize)
+ * (out/external/MixedKernelListDecoder.cpp:9): spec is the text of the reference's code
+ * specification (out/external/MixedKernelEncoder.cpp:7-98: "N K d layers #shortened
+ * #punctured", kernel names, shortened / punctured symbols, U - K freezing constraints).
+ * The GPU decoder takes Arikan ("A") layers, 1 <= list_size <= 32, and lengths whose
+ * per-wave state fits the 160 KiB LDS (U <= 1024 at L = 16, 2048 at L = 8). */
+int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **out);
+void bchk_polar_destroy(bchk_polar *pc);
+/* N (transmitted length), K, U (unshortened length), L */
+int bchk_polar_params(const bchk_polar *pc, int *n, int *k, int *unshortened, int *list_size);
+/* Replaces Decode(pLLR, pInfVectorList, pCodewordList) (MixedKernelListDecoder.cpp:211-268),
+ * batched: llr [B][N] float, log P(0)/P(1) as the decoder reads them (bit 1 when < 0);
+ * per codeword the list, best path first: info [B][L][K], cw [B][L][N] (may be NULL),
+ * metric [B][L] (path metrics, 0 = the hard decision), count [B] (rows written; rows past
+ * it are left as they were). */
+int bchk_polar_decode_host(bchk_polar *pc, const float *llr, size_t B, uint8_t *info,
+                           uint8_t *cw, float *metric, int32_t *count);
+int bchk_polar_decode_device(bchk_polar *pc, const float *d_llr, size_t B, uint8_t *d_info,
+                             uint8_t *d_cw, float *d_metric, int32_t *d_count, void *stream);
+/* CMixedKernelEncoder::Encode (MixedKernelEncoder.cpp:142-177), host side: info [B][K] ->
+ * codewords [B][N]. */
+int bchk_polar_encode_host(const bchk_polar *pc, const uint8_t *info, size_t B, uint8_t *cw);
+int bchk_polar_sync(bchk_polar *pc);
+void *bchk_polar_stream(bchk_polar *pc);
+
 const char *bchk_last_error(void);
 const char *bchk_version(void);
 

@@ -33,7 +33,9 @@ EXPORTS = (
     "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device",
     "bchk_generate_host", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
     "bchk_profile_read", "bchk_path_counts", "bchk_set_fast_path", "bchk_set_syndrome_table",
-    "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_last_error", "bchk_version",
+    "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_polar_create",
+    "bchk_polar_destroy", "bchk_polar_params", "bchk_polar_decode_host", "bchk_polar_decode_device",
+    "bchk_polar_encode_host", "bchk_polar_sync", "bchk_polar_stream", "bchk_last_error", "bchk_version",
 )
 
 STATS_DTYPE = np.dtype([("decodes", "<u8"), ("comparisons", "<u8"), ("sums", "<u8"),
@@ -91,6 +93,16 @@ def lib():
     L.bchk_profile_read.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
     L.bchk_set_fast_path.argtypes = [vp, i32]
     L.bchk_set_syndrome_table.argtypes = [vp, i32]
+    L.bchk_polar_create.argtypes = [C.c_char_p, i32, i32, C.POINTER(vp)]
+    L.bchk_polar_destroy.argtypes = [vp]
+    L.bchk_polar_destroy.restype = None
+    L.bchk_polar_params.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
+    L.bchk_polar_decode_host.argtypes = [vp, vp, sz, vp, vp, vp, vp]
+    L.bchk_polar_decode_device.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
+    L.bchk_polar_encode_host.argtypes = [vp, vp, sz, vp]
+    L.bchk_polar_sync.argtypes = [vp]
+    L.bchk_polar_stream.argtypes = [vp]
+    L.bchk_polar_stream.restype = vp
     L.bchk_syndrome_table_query.argtypes = [i32, i32, vp, sz, vp, vp]
     L.bchk_syndrome_table_info.argtypes = [i32, i32, C.POINTER(u64), C.POINTER(u64),
                                            C.POINTER(C.c_uint32)]
@@ -225,6 +237,63 @@ class KanekoKernelProcessor:
     def set_syndrome_table(self, enable=True):
         """Syndrome decoding table of the search kernels (results identical either way)."""
         _check(lib().bchk_set_syndrome_table(self._h, 1 if enable else 0))
+
+
+class PolarListDecoder:
+    """CMixedKernelListDecoder(Spec, ListSize) + Decode (out/external/MixedKernelListDecoder.cpp
+    :9, :211-268) on the GPU: batched SC-list decoding of a polar code given by the
+    reference's specification text (Arikan layers)."""
+
+    def __init__(self, spec, L, device=0):
+        h = C.c_void_p()
+        _check(lib().bchk_polar_create(spec.encode(), L, device, C.byref(h)))
+        self._h = h
+        n, k, u, l = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        _check(lib().bchk_polar_params(h, C.byref(n), C.byref(k), C.byref(u), C.byref(l)))
+        self.N, self.K, self.U, self.L = n.value, k.value, u.value, l.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().bchk_polar_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self):
+        return lib().bchk_polar_stream(self._h)
+
+    def encode(self, info):
+        info = np.ascontiguousarray(info, np.uint8)
+        cw = np.zeros((info.shape[0], self.N), np.uint8)
+        _check(lib().bchk_polar_encode_host(self._h, _p(info), info.shape[0], _p(cw)))
+        return cw
+
+    def decode(self, llr):
+        """llr [B][N] float32 -> (count [B], info [B][L][K], codewords [B][L][N], metrics [B][L])."""
+        llr = np.ascontiguousarray(llr, np.float32)
+        B = llr.shape[0]
+        info = np.zeros((B, self.L, self.K), np.uint8)
+        cw = np.zeros((B, self.L, self.N), np.uint8)
+        met = np.zeros((B, self.L), np.float32)
+        cnt = np.zeros(B, np.int32)
+        _check(lib().bchk_polar_decode_host(self._h, _p(llr), B, _p(info), _p(cw), _p(met), _p(cnt)))
+        return cnt, info, cw, met
+
+    def decode_device(self, d_llr, B, d_info, d_cw, d_metric, d_count, stream=None):
+        _check(lib().bchk_polar_decode_device(self._h, d_llr, B, d_info, d_cw, d_metric, d_count,
+                                              stream))
+
+    def sync(self):
+        _check(lib().bchk_polar_sync(self._h))
 
 
 def syndrome_table_query(m, t, syndromes):

@@ -237,8 +237,9 @@ kaneko_fast_kernel(SearchParams p) {
         double g[LMAX];
         uint64_t v = diff;
 #pragma unroll
-        for (int j = 0; j < LMAX; ++j) {  // independent loads, issued together
-            g[j] = yrow[v ? (int)__builtin_ctzll(v) : 0];
+        for (int j = 0; j < LMAX; ++j) {  // independent loads, issued together; only the
+            g[j] = 0.0;                    // flipped positions' (no line fetched for others)
+            if (v) g[j] = yrow[(int)__builtin_ctzll(v)];
             v &= v - 1;
         }
         l = 0.0;

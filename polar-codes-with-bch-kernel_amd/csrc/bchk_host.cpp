@@ -549,6 +549,10 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
 
 }  // namespace
 
+namespace bchk {
+void set_last_error(const char *msg) { g_err = msg; }  // for polar_host.cpp
+}  // namespace bchk
+
 extern "C" {
 
 const char *bchk_last_error(void) { return g_err.c_str(); }
@@ -947,7 +951,6 @@ int bchk_syndrome_table_query(int m, int t, const uint32_t *synd, size_t N, uint
     if (int rc = host_table(f, t, &h)) return rc;
     TableDesc td{};
     const std::vector<uint8_t> blob = make_tables(f, t, &td);
-    const uint8_t *ex = blob.data() + td.off_exp;
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(blob.data() + td.off_log);
     SyndTable T{h->slots.data(), h->bbits, h->max_probe};
     for (size_t i = 0; i < N; ++i) {
