@@ -16,28 +16,31 @@ struct PolarParams {
     float *metric;          // [B][L] path metrics
     int32_t *count;         // [B] list entries written
     const int16_t *symmap;  // [U] LoadLLRs: index into the LLR row; -1 shortened, -2 punctured
-    const uint8_t *frozen;  // [U] 1 = (dynamic) frozen symbol
-    const int8_t *dfbit;    // [U] mask bit holding a frozen symbol's value, -1 = static
+    const uint16_t *phase;  // [U] bit 0 frozen | (dynamic-freezing bit + 1) << 1 | has-correction << 8
     const uint64_t *dfcorr; // [U] dynamic-freezing correction masks
-    const int16_t *infopos; // [K] unfrozen symbols
     const int16_t *cwpos;   // [N] transmitted (neither shortened nor punctured) symbols
     uint32_t B;
     int32_t n, U, N, K, L;
 };
 
-// LDS bytes of one wave's state (see polar_sclist.hip): channel LLRs, per path S (U floats,
-// padded) and C (3U bytes, padded) arrays, per path metric / LLR / mask, the path stack,
-// the list of active paths and a U-byte scratch row.
-inline uint32_t polar_lds_bytes(int U, int L) {
-    uint32_t b = 4u * (uint32_t)U;                  // channel
-    b += 4u * (uint32_t)U * (uint32_t)L;            // S
-    b += 4u * (uint32_t)L * 2u;                     // R, llr
-    b = (b + 7u) & ~7u;
-    b += 8u * (uint32_t)L;                          // DF masks
-    b += 4u * (uint32_t)(L + 1) + 4u * (uint32_t)L; // stack, active list
+constexpr uint16_t kPhaseFrozen = 1u, kPhaseCorr = 0x100u;
+
+// (constexpr: usable from device code too.) Per-path strides in LDS, padded by 16 bytes so that the same element of consecutive paths
+// falls in different banks (64 x 4 B banks): S holds U floats, C 3U bytes.
+constexpr int polar_path_s(int U) { return ((U + 3) & ~3) + 4; }
+constexpr int polar_path_c(int U) { return ((3 * U + 15) & ~15) + 16; }
+constexpr int polar_rec_words(int K) { return K > 0 ? (K + 31) / 32 : 1; }
+
+// LDS bytes of one wave's state (see polar_sclist.hip): channel LLRs, per path S and C,
+// the phase table, the active-path list and per path the information bits decided so far.
+inline uint32_t polar_lds_bytes(int U, int L, int K) {
+    uint32_t b = (4u * (uint32_t)U + 15u) & ~15u;                     // channel
+    b += 4u * (uint32_t)polar_path_s(U) * (uint32_t)L;                // S
+    b += (uint32_t)polar_path_c(U) * (uint32_t)L;                     // C
+    b += 2u * (uint32_t)U;                                            // phase table
     b = (b + 15u) & ~15u;
-    b += 3u * (uint32_t)U * (uint32_t)L;            // C
-    b += (uint32_t)U;                               // scratch
+    b += 4u * (uint32_t)L;                                            // active list
+    b += 4u * (uint32_t)L * (uint32_t)polar_rec_words(K);             // information bits
     return (b + 15u) & ~15u;
 }
 

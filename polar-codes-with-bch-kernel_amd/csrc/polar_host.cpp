@@ -76,8 +76,8 @@ struct bchk_polar {
     std::vector<uint64_t> dfcorr;
     std::vector<std::vector<int>> fc;  // freezing constraints (terms, frozen symbol last)
     std::vector<int> decision;         // constraint of each symbol, -1 = unfrozen
-    uint8_t *d_tab = nullptr;          // one blob: symmap | frozen | dfbit | infopos | cwpos | dfcorr
-    size_t off_symmap = 0, off_frozen = 0, off_dfbit = 0, off_infopos = 0, off_cwpos = 0, off_dfcorr = 0;
+    uint8_t *d_tab = nullptr;          // one blob: symmap | phase | cwpos | dfcorr
+    size_t off_symmap = 0, off_phase = 0, off_cwpos = 0, off_dfcorr = 0;
     hipStream_t stream = nullptr;
     size_t lds = 0;
     int grid = 0;
@@ -179,7 +179,7 @@ int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **
         delete c;
         return rc;
     }
-    c->lds = polar_lds_bytes(c->U, c->L);
+    c->lds = polar_lds_bytes(c->U, c->L, c->K);
     if (c->lds > 160 * 1024) {
         const size_t need = c->lds;
         const int U = c->U;
@@ -208,16 +208,17 @@ int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **
     auto al = [](size_t v) { return (v + 15) & ~size_t(15); };
     size_t o = 0;
     c->off_symmap = o; o = al(o + 2 * (size_t)c->U);
-    c->off_frozen = o; o = al(o + (size_t)c->U);
-    c->off_dfbit = o; o = al(o + (size_t)c->U);
-    c->off_infopos = o; o = al(o + 2 * (size_t)std::max(c->K, 1));
+    c->off_phase = o; o = al(o + 2 * (size_t)c->U);
     c->off_cwpos = o; o = al(o + 2 * (size_t)c->N);
     c->off_dfcorr = o; o = al(o + 8 * (size_t)c->U);
     std::vector<uint8_t> blob(o, 0);
     memcpy(blob.data() + c->off_symmap, c->symmap.data(), 2 * (size_t)c->U);
-    memcpy(blob.data() + c->off_frozen, c->frozen.data(), (size_t)c->U);
-    memcpy(blob.data() + c->off_dfbit, c->dfbit.data(), (size_t)c->U);
-    if (c->K) memcpy(blob.data() + c->off_infopos, c->infopos.data(), 2 * (size_t)c->K);
+    {
+        uint16_t *ph = reinterpret_cast<uint16_t *>(blob.data() + c->off_phase);
+        for (int i = 0; i < c->U; ++i)
+            ph[i] = (uint16_t)((c->frozen[i] ? kPhaseFrozen : 0u) | ((uint16_t)(c->dfbit[i] + 1) << 1) |
+                               (c->dfcorr[i] ? kPhaseCorr : 0u));
+    }
     memcpy(blob.data() + c->off_cwpos, c->cwpos.data(), 2 * (size_t)c->N);
     memcpy(blob.data() + c->off_dfcorr, c->dfcorr.data(), 8 * (size_t)c->U);
     if (hipMalloc(&c->d_tab, o) != hipSuccess ||
@@ -234,6 +235,10 @@ int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **
         (void)hipGetLastError();
     }
     c->grid = per_cu * prop.multiProcessorCount;
+    if (const char *g = getenv("BCHK_POLAR_GRID")) c->grid = std::max(1, atoi(g));
+    if (getenv("BCHK_POLAR_DEBUG"))
+        fprintf(stderr, "bchk_polar: U=%d L=%d lds=%u per_cu=%d CUs=%d grid=%d\n", c->U, c->L, c->lds, per_cu,
+                prop.multiProcessorCount, c->grid);
     *out = c;
     return 0;
 }
@@ -271,9 +276,7 @@ int bchk_polar_decode_device(bchk_polar *c, const float *d_llr, size_t B, uint8_
     p.metric = d_metric;
     p.count = d_count;
     p.symmap = reinterpret_cast<const int16_t *>(c->d_tab + c->off_symmap);
-    p.frozen = c->d_tab + c->off_frozen;
-    p.dfbit = reinterpret_cast<const int8_t *>(c->d_tab + c->off_dfbit);
-    p.infopos = reinterpret_cast<const int16_t *>(c->d_tab + c->off_infopos);
+    p.phase = reinterpret_cast<const uint16_t *>(c->d_tab + c->off_phase);
     p.cwpos = reinterpret_cast<const int16_t *>(c->d_tab + c->off_cwpos);
     p.dfcorr = reinterpret_cast<const uint64_t *>(c->d_tab + c->off_dfcorr);
     p.B = (uint32_t)B;

@@ -8,16 +8,18 @@
 // arithmetic and the same path indices (the list sorts break ties on them), so the output
 // lists equal the CPU restatement (oracle/polar_oracle.c) bit for bit.
 //
-// Execution model: one 64-lane wave per codeword (persistent over the batch), every path's
-// state in LDS. Layer λ of path p keeps its LLRs S_λ (U >> λ floats) and partial sums C_λ
-// (kernel inputs of the current block, U >> (λ-1) bytes; C_0 = the codeword). Each phase:
-//   * the LLR recursion from the first layer whose block changed, lanes over
-//     (active path x element);
-//   * decisions: frozen symbols per path (lane = path); unfrozen ones rank the 2 L
-//     candidates (lane = path x bit) with the reference's std::greater<pair> order,
-//     then kills and clones run wave-uniformly in path order (clone = LDS copy of the
-//     parent's arrays);
-//   * the partial-sum butterflies of the finished blocks.
+// Execution model: one 64-lane wave per codeword (persistent over the batch).
+//   * LDS holds every path's LLRs S_λ (U >> λ floats) and partial sums C_λ (kernel inputs
+//     of the current block, U >> (λ-1) bytes; C_0 = the codeword), the phase table and the
+//     information bits decided so far (packed, flushed every 32 decisions).
+//   * Lane q < L holds path q's scalar state in registers: metric R, leaf LLR, dynamic-
+//     freezing mask, the current record word and slot q of the path-index stack (pushes and
+//     pops are v_writelane / v_readlane on a wave-uniform top).
+//   * Each phase: the LLR recursion from the first layer whose block changed, lanes over
+//     (active path x element); decisions (frozen: lane = path; unfrozen: the 2 L candidates
+//     ranked in lanes 2q + b with the reference's std::greater<pair> order); kills, then
+//     clones in path order, a clone copying only the parent's live S layers, live C halves
+//     and record words; then the partial-sum butterflies of the finished blocks.
 // No MFMA: the work is float min/add and byte XOR on short vectors.
 #include <hip/hip_runtime.h>
 
@@ -28,6 +30,8 @@
 namespace bchk {
 
 namespace {
+
+constexpr uint32_t kUninit = 0xFFFFFFFFu;
 
 __device__ __forceinline__ void wave_sync_p() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -51,35 +55,38 @@ __device__ __forceinline__ float f_minsum(float a, float b) {
 __device__ __forceinline__ float rdl_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+__device__ __forceinline__ uint32_t rdl_u(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t rdl_u64(uint64_t v, int l) {
+    return (uint64_t)rdl_u((uint32_t)v, l) | ((uint64_t)rdl_u((uint32_t)(v >> 32), l) << 32);
+}
 
-// The path stack of TVMemoryEngine (headers/external/misc.h:212-226), in LDS: every lane
-// reads, lane 0 writes.
-__device__ __forceinline__ uint32_t st_pop(uint32_t *s, int lane) {
-    const uint32_t top = s[0], v = s[top];
-    uint32_t r;
-    wave_sync_p();
-    if (v == 0xFFFFFFFFu) {  // not yet initialised: hand out top - 1
-        r = top - 1u;
-        if (lane == 0) {
-            s[0] = r;
-            if (r > 0) s[r] = 0xFFFFFFFFu;
+// The path-index stack of TVMemoryEngine (headers/external/misc.h:212-226) with its lazy
+// initialisation: slot i lives in lane i's `slot`, `top` is wave-uniform.
+struct PathStack {
+    uint32_t slot;
+    int top;
+    __device__ __forceinline__ void reset(int L, int lane) {
+        top = L;
+        if (lane == L) slot = kUninit;
+    }
+    __device__ __forceinline__ uint32_t pop(int lane) {
+        const uint32_t v = rdl_u(slot, top);
+        if (v == kUninit) {  // never pushed: hand out top - 1
+            const int r = top - 1;
+            top = r;
+            if (r > 0 && lane == r) slot = kUninit;
+            return (uint32_t)r;
         }
-    } else {
-        r = v;
-        if (lane == 0) s[0] = top - 1u;
+        --top;
+        return v;
     }
-    wave_sync_p();
-    return r;
-}
-__device__ __forceinline__ void st_push(uint32_t x, uint32_t *s, int lane) {
-    const uint32_t top = s[0] + 1u;
-    wave_sync_p();
-    if (lane == 0) {
-        s[top] = x;
-        s[0] = top;
+    __device__ __forceinline__ void push(uint32_t x, int lane) {
+        ++top;
+        if (lane == top) slot = x;
     }
-    wave_sync_p();
-}
+};
 
 // act[k] = index of the k-th active path; returns their number
 __device__ __forceinline__ int list_active(uint32_t active, uint32_t *act, int lane, int L) {
@@ -93,22 +100,28 @@ __device__ __forceinline__ int list_active(uint32_t active, uint32_t *act, int l
 __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = (int)threadIdx.x;
-    const int U = p.U, n = p.n, L = p.L;
-    const int pathS = U, pathC = 3 * U;  // padded per-path strides (floats, bytes)
+    const int U = p.U, n = p.n, L = p.L, K = p.K;
+    const int pathS = polar_path_s(U), pathC = polar_path_c(U), RW = polar_rec_words(K);
     // LDS layout: polar_lds_bytes (polar_device.h)
+    // (byte offsets from smem, never through integer casts of the pointers, which would
+    // lose the LDS address space and turn every access into a FLAT one)
+    const int o_S = (4 * U + 15) & ~15;
+    const int o_C = o_S + 4 * pathS * L;
+    const int o_ph = o_C + pathC * L;
+    const int o_act = (o_ph + 2 * U + 15) & ~15;
     float *chan = reinterpret_cast<float *>(smem);
-    float *S = chan + U;
-    float *Rv = S + (size_t)pathS * L;
-    float *lv = Rv + L;
-    uintptr_t a8 = (reinterpret_cast<uintptr_t>(lv + L) + 7u) & ~uintptr_t(7);
-    uint64_t *dfm = reinterpret_cast<uint64_t *>(a8);
-    uint32_t *stack = reinterpret_cast<uint32_t *>(dfm + L);
-    uint32_t *act = stack + L + 1;
-    uintptr_t a16 = (reinterpret_cast<uintptr_t>(act + L) + 15u) & ~uintptr_t(15);
-    uint8_t *C = reinterpret_cast<uint8_t *>(a16);
-    uint8_t *tmp = C + (size_t)pathC * L;
+    float *S = reinterpret_cast<float *>(smem + o_S);
+    uint8_t *C = smem + o_C;
+    uint16_t *ph = reinterpret_cast<uint16_t *>(smem + o_ph);
+    uint32_t *act = reinterpret_cast<uint32_t *>(smem + o_act);
+    uint32_t *rec = act + L;
     const int lastc = c_off(U, n);  // C_n: the two inputs of the last Arikan block
+    const bool mine = lane < L;
 
+    for (int i = lane; i < U; i += 64) ph[i] = p.phase[i];
+
+    PathStack st;
+    st.slot = 0;
     for (uint32_t cw = blockIdx.x; cw < p.B; cw += gridDim.x) {
         // ---- LoadLLRs (MixedKernelEncoder.cpp:181-207)
         const float *y = p.llr + (size_t)cw * p.N;
@@ -117,27 +130,23 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
             chan[i] = m >= 0 ? y[m] : (m == -1 ? 100000.0f : 0.0f);
         }
         // ---- Cleanup + AssignInitialPath (TVMemoryEngine.cpp:58-94)
-        if (lane == 0) {
-            stack[0] = (uint32_t)L;
-            stack[L] = 0xFFFFFFFFu;
-        }
-        wave_sync_p();
-        const uint32_t pid = st_pop(stack, lane);
+        st.reset(L, lane);
+        const uint32_t pid = st.pop(lane);
         uint32_t active = 1u << pid;
-        if (lane == 0) {
-            Rv[pid] = 0.0f;
-            dfm[pid] = 0ull;
-        }
+        float R = 0.0f, lv = 0.0f;
+        uint64_t dm = 0;
+        uint32_t rw = 0;
+        int k = 0;  // unfrozen decisions so far
         wave_sync_p();
         int nact = list_active(active, act, lane, L);
 
         for (int phi = 0; phi < U; ++phi) {
+            const uint32_t e = __builtin_amdgcn_readfirstlane((uint32_t)ph[phi]);
             // ---- IterativelyCalcS (KernelListEngine.cpp:370-447): from layer m, where the
             // block of phase phi starts, down to the single LLR of layer n
             int m = 0, local = 0;
             if (phi) {
-                const int tz = __builtin_ctz((unsigned)phi);
-                m = n - 1 - tz;
+                m = n - 1 - __builtin_ctz((unsigned)phi);
                 local = 1;
             }
             for (int j = m; j < n; ++j) {
@@ -160,32 +169,26 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
                 }
                 wave_sync_p();
             }
-            if (lane < L && ((active >> lane) & 1u)) lv[lane] = S[(size_t)lane * pathS + U - 2];
-            wave_sync_p();
+            const bool on = mine && ((active >> lane) & 1u);
+            if (on) lv = S[(size_t)lane * pathS + U - 2];
+            const uint64_t corr = (e & kPhaseCorr) ? p.dfcorr[phi] : 0ull;
+            uint32_t dec = 0;
 
-            if (p.frozen[phi]) {
+            if (e & kPhaseFrozen) {
                 // ---- ContinuePathsFrozen (MixedKernelListDecoder.cpp:61-98)
-                const int db = p.dfbit[phi];
-                const uint64_t corr = p.dfcorr[phi];
-                if (lane < L && ((active >> lane) & 1u)) {
-                    const float v = lv[lane];
-                    const int cb = db >= 0 ? (int)((dfm[lane] >> db) & 1ull) : 0;
-                    if ((cb > 0) ^ (v < 0.0f)) Rv[lane] -= fabsf(v);
-                    C[(size_t)lane * pathC + lastc + (phi & 1)] = (uint8_t)cb;
-                    if (cb) dfm[lane] ^= corr;
+                const int db = (int)((e >> 1) & 127u) - 1;
+                if (on) {
+                    dec = db >= 0 ? (uint32_t)((dm >> db) & 1ull) : 0u;
+                    if ((dec != 0) ^ (lv < 0.0f)) R -= fabsf(lv);
                 }
-                wave_sync_p();
             } else {
                 // ---- ContinuePathsUnfrozen (:100-185). Candidate 2q + b (bit b of path q)
                 // sits in lane 2q + b; its score is R (b = hard decision) or R - |llr|.
                 const int q = lane >> 1, b = lane & 1;
+                const float vq = __shfl(lv, q & 31), Rq = __shfl(R, q & 31);
                 const bool valid = q < L && ((active >> q) & 1u);
                 float sc = 0.0f;
-                if (valid) {
-                    const float v = lv[q];
-                    const int hd = v < 0.0f;
-                    sc = (b == hd) ? Rv[q] : Rv[q] - fabsf(v);
-                }
+                if (valid) sc = (b == (vq < 0.0f ? 1 : 0)) ? Rq : Rq - fabsf(vq);
                 // rank under std::greater<pair<float, unsigned>> (:125): score, then index
                 int rank = 0;
                 for (uint64_t mm = __ballot(valid); mm; mm &= mm - 1) {
@@ -195,58 +198,81 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
                 }
                 const int J = 2 * nact, keep = J < L ? J : L;
                 const uint64_t sel = __ballot(valid && rank < keep);
-                const uint64_t corr = p.dfcorr[phi];
-                for (int i = 0; i < L; ++i)  // KillPath, in path order (:129-136)
-                    if (((active >> i) & 1u) && !((sel >> (2 * i)) & 3ull)) {
-                        st_push((uint32_t)i, stack, lane);
-                        active &= ~(1u << i);
+                const uint32_t cont = mine ? (uint32_t)((sel >> (2 * lane)) & 3ull) : 0u;
+                const uint32_t cont_any = (uint32_t)__ballot(cont != 0);
+                const uint32_t clones = (uint32_t)__ballot(cont == 3u);
+                // KillPath, in path order (:129-136)
+                for (uint32_t kill = active & ~cont_any; kill; kill &= kill - 1) st.push((uint32_t)__builtin_ctz(kill), lane);
+                active &= cont_any;
+                // continuations (:138-178): 1 -> bit 0, 2 -> bit 1, 3 -> the hard decision
+                // here and its complement in a clone; the score changes only in the clone
+                dec = cont == 2u ? 1u : (cont == 3u ? (lv < 0.0f ? 1u : 0u) : 0u);
+                for (uint32_t cl = clones; cl; cl &= cl - 1) {
+                    const int l = __builtin_ctz(cl);
+                    const int l1 = (int)st.pop(lane);  // ClonePath: copy the live state of l
+                    {
+                        // S_j (j >= 1) is read again iff bit n-1-j of phi is 0; copy from the
+                        // first such layer on. Left halves of C_λ are pending iff bit n-λ of
+                        // phi is 1; copy from the first such λ on.
+                        const uint32_t zs = ~(uint32_t)phi & ((1u << (n - 1)) - 1u);
+                        const int s0 = zs ? (s_off(U, n - 1 - (31 - __builtin_clz(zs))) & ~3) : pathS;
+                        const int ns4 = (((U + 3) & ~3) - s0) >> 2;
+                        const int c0 = phi ? (c_off(U, n - (31 - __builtin_clz((uint32_t)phi))) & ~15) : pathC;
+                        const int nc16 = (((3 * U + 15) & ~15) - c0) >> 4;
+                        const int nr = k >> 5;
+                        const uint4 *sS = reinterpret_cast<const uint4 *>(S + (size_t)l * pathS + s0);
+                        uint4 *dS = reinterpret_cast<uint4 *>(S + (size_t)l1 * pathS + s0);
+                        const uint4 *sC = reinterpret_cast<const uint4 *>(C + (size_t)l * pathC + c0);
+                        uint4 *dC = reinterpret_cast<uint4 *>(C + (size_t)l1 * pathC + c0);
+                        const int top = ns4 > nc16 ? ns4 : nc16;
+                        for (int i = lane; i < top || i < nr; i += 64) {
+                            uint4 vs, vc;
+                            uint32_t vr = 0;
+                            if (i < ns4) vs = sS[i];
+                            if (i < nc16) vc = sC[i];
+                            if (i < nr) vr = rec[l * RW + i];
+                            if (i < ns4) dS[i] = vs;
+                            if (i < nc16) dC[i] = vc;
+                            if (i < nr) rec[l1 * RW + i] = vr;
+                        }
                     }
-                for (int l = 0; l < L; ++l) {  // continuations, in path order (:138-178)
-                    const int cont = (int)((sel >> (2 * l)) & 3ull);
-                    if (!cont) continue;
-                    uint8_t *cl = C + (size_t)l * pathC + lastc + (phi & 1);
-                    if (cont == 1) {
-                        if (lane == 0) *cl = 0;
-                    } else if (cont == 2) {
-                        if (lane == 0) {
-                            *cl = 1;
-                            dfm[l] ^= corr;
-                        }
-                    } else {
-                        const float v = lv[l];
-                        const uint8_t cb = v < 0.0f;
-                        if (lane == 0) *cl = cb;
-                        wave_sync_p();
-                        const uint32_t l1 = st_pop(stack, lane);  // ClonePath
-                        {
-                            const uint32_t *s4 = reinterpret_cast<const uint32_t *>(S + (size_t)l * pathS);
-                            uint32_t *d4 = reinterpret_cast<uint32_t *>(S + (size_t)l1 * pathS);
-                            for (int i = lane; i < pathS; i += 64) d4[i] = s4[i];
-                            const uint32_t *c4 = reinterpret_cast<const uint32_t *>(C + (size_t)l * pathC);
-                            uint32_t *e4 = reinterpret_cast<uint32_t *>(C + (size_t)l1 * pathC);
-                            for (int i = lane; i < pathC / 4; i += 64) e4[i] = c4[i];
-                        }
-                        wave_sync_p();
-                        if (lane == 0) {
-                            C[(size_t)l1 * pathC + lastc + (phi & 1)] = (uint8_t)(cb ^ 1u);
-                            Rv[l1] = Rv[l] - fabsf(v);
-                            const uint64_t dm = dfm[l];
-                            dfm[l1] = cb ? dm : dm ^ corr;
-                            dfm[l] = cb ? dm ^ corr : dm;
-                        }
-                        active |= 1u << l1;
+                    const float Rl = rdl_f(R, l), vl = rdl_f(lv, l);
+                    const uint64_t dml = rdl_u64(dm, l);
+                    const uint32_t rwl = rdl_u(rw, l), decl = rdl_u(dec, l);
+                    if (lane == l1) {
+                        R = Rl - fabsf(vl);
+                        dm = dml;
+                        rw = rwl;
+                        dec = decl ^ 1u;
+                        lv = vl;
                     }
-                    wave_sync_p();
+                    active |= 1u << l1;
+                }
+                wave_sync_p();
+            }
+            const bool now = mine && ((active >> lane) & 1u);
+            if (now) {
+                C[(size_t)lane * pathC + lastc + (phi & 1)] = (uint8_t)dec;
+                if (dec) dm ^= corr;
+            }
+            if (!(e & kPhaseFrozen)) {
+                if (now) rw |= dec << (k & 31);
+                ++k;
+                if ((k & 31) == 0) {
+                    if (now) rec[lane * RW + (k >> 5) - 1] = rw;
+                    rw = 0;
                 }
                 nact = list_active(active, act, lane, L);
+            } else {
+                wave_sync_p();
             }
 
             // ---- IterativelyUpdateC (KernelListEngine.cpp:266-315): the blocks this phase
             // completes are encoded into their parents' slots
             {
-                int lam = n, lgs = 0, ph = phi;
-                while (lam > 0 && (ph & 1)) {
-                    const int psi = ph >> 1;
+                int lam = n, lgs = 0, ph2 = phi;
+                while (lam > 0 && (ph2 & 1)) {
+                    const int psi = ph2 >> 1;
                     const int stride = 1 << lgs, next = stride << 1;
                     const int phi0 = (lam > 1) ? (psi & 1) * next : 0;
                     const int tot = nact << lgs;
@@ -260,45 +286,50 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
                     }
                     wave_sync_p();
                     ++lgs;
-                    ph = psi;
+                    ph2 = psi;
                     --lam;
                 }
             }
         }
+        if ((k & 31) && mine && ((active >> lane) & 1u)) rec[lane * RW + (k >> 5)] = rw;
+        wave_sync_p();
 
         // ---- final order (:249-267): active paths by (R, index), descending
         int rk = 0;
-        float rv = 0.0f;
-        const bool me = lane < L && ((active >> lane) & 1u);
-        if (me) rv = Rv[lane];
+        const bool me = mine && ((active >> lane) & 1u);
         for (uint64_t mm = __ballot(me); mm; mm &= mm - 1) {
             const int o = (int)__builtin_ctzll(mm);
-            const float ro = rdl_f(rv, o);
-            rk += (rv < ro || (!(ro < rv) && lane < o)) ? 1 : 0;
+            const float ro = rdl_f(R, o);
+            rk += (R < ro || (!(ro < R) && lane < o)) ? 1 : 0;
         }
-        const uint64_t mme = __ballot(me);
         for (int r = 0; r < nact; ++r) {
-            const uint64_t who = __ballot(me && rk == r);
-            const int q = (int)__builtin_ctzll(who);
+            const int q = (int)__builtin_ctzll(__ballot(me && rk == r));
             const uint8_t *cq = C + (size_t)q * pathC;  // C_0: the unshortened codeword
-            // information bits: the inverse transform (= the transform, stages commute)
-            for (int i = lane; i < U; i += 64) tmp[i] = cq[i];
-            wave_sync_p();
-            for (int st = 1; st < U; st <<= 1) {
-                for (int i = lane; i < U / 2; i += 64) {
-                    const int lo = ((i & ~(st - 1)) << 1) | (i & (st - 1));
-                    tmp[lo] ^= tmp[lo + st];
-                }
-                wave_sync_p();
-            }
+            const uint32_t *rq = rec + q * RW;
             const size_t row = (size_t)cw * L + r;
-            for (int k = lane; k < p.K; k += 64) p.info[row * p.K + k] = tmp[p.infopos[k]];
-            if (p.cw)
-                for (int i = lane; i < p.N; i += 64) p.cw[row * p.N + i] = cq[p.cwpos[i]];
-            if (lane == 0) p.metric[row] = Rv[q];
-            wave_sync_p();
+            if ((K & 3) == 0) {  // information bits, four per lane and store
+                uint32_t *o4 = reinterpret_cast<uint32_t *>(p.info + row * K);
+                for (int w = lane; w < (K >> 2); w += 64) {
+                    const uint32_t bits = (rq[w >> 3] >> ((w & 7) * 4)) & 15u;
+                    o4[w] = (bits & 1u) | ((bits & 2u) << 7) | ((bits & 4u) << 14) | ((bits & 8u) << 21);
+                }
+            } else {
+                for (int kk = lane; kk < K; kk += 64) p.info[row * K + kk] = (uint8_t)((rq[kk >> 5] >> (kk & 31)) & 1u);
+            }
+            if (p.cw) {
+                if ((p.N & 3) == 0) {
+                    uint32_t *o4 = reinterpret_cast<uint32_t *>(p.cw + row * p.N);
+                    for (int w = lane; w < (p.N >> 2); w += 64) {
+                        const int i0 = 4 * w;
+                        o4[w] = (uint32_t)cq[p.cwpos[i0]] | ((uint32_t)cq[p.cwpos[i0 + 1]] << 8) |
+                                ((uint32_t)cq[p.cwpos[i0 + 2]] << 16) | ((uint32_t)cq[p.cwpos[i0 + 3]] << 24);
+                    }
+                } else {
+                    for (int i = lane; i < p.N; i += 64) p.cw[row * p.N + i] = cq[p.cwpos[i]];
+                }
+            }
+            if (lane == 0) p.metric[row] = rdl_f(R, q);
         }
-        (void)mme;
         if (lane == 0) p.count[cw] = nact;
         wave_sync_p();
     }
