@@ -197,11 +197,16 @@ def main():
     launches = max(1, launches)
     pipe = max(1, launches // args.steps)  # sub-batches per decode call (stream pipeline)
     tm = dec_tmax(args.t)
-    fast_on = ms3[0] > 0 and n_exact < B
+    # the lane-per-codeword fast kernel exists for n <= 63 and small t (csrc/bchk_fast.hip
+    # select_fast); without it stage 0 is only the control-block memset
+    # (n > 63: kaneko_first_kernel, the first test patterns of every codeword)
+    has_fast = args.m >= 7 or args.t <= {3: 3, 4: 7, 5: 8, 6: 6}.get(args.m, -1)
+    fast_name = "kaneko_fast_kernel" if args.m <= 6 else "kaneko_first_kernel"
+    fast_on = has_fast and ms3[0] > 0 and n_exact < B
     # per launch: average duration (HIP events on the launching stream) and the codewords
     # one launch processes (the last call's hand-off counts, spread over its sub-batches)
-    kern = [{"name": f"kaneko_fast_kernel<{args.m},{tm}>", "ms": ms3[0] / launches,
-             "codewords": B / pipe},
+    kern = [{"name": f"{fast_name}<{args.m},{tm}>" if has_fast else "control memset",
+             "ms": ms3[0] / launches, "codewords": B / pipe if has_fast else 0},
             {"name": f"kaneko_search_kernel<{args.m},{tm}>", "ms": ms3[1] / launches,
              "codewords": (n_exact if fast_on else B) / pipe},
             {"name": f"kaneko_coop_kernel<{args.m},{tm}>", "ms": ms3[2] / launches,

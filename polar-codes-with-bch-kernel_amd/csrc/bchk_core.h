@@ -96,13 +96,13 @@ __device__ __forceinline__ int mask_popc(const Mask<NW> &m) {
 // syndromes Sw (byte j = S_{2j+1}). Success iff the syndrome is nonzero, the BM register
 // length L <= t and the locator has deg C >= 1 distinct roots in GF(2^m)*; E = flipped
 // positions ((n - k) mod n for each root alpha^k, :287).
+// Inversionless binary Berlekamp-Massey over the table GF(2^m): connection polynomial C
+// (TMAX + 1 coefficients) and register length L of the syndromes S_1 .. S_2t.
 template <int M, int TMAX>
-__device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
-                                         const uint16_t *__restrict__ lg,
-                                         const uint64_t *__restrict__ chien,
-                                         const uint32_t *Sw, int t,
-                                         Mask<Geo<M>::NW> &E) {
-    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL, NW = Geo<M>::NW;
+__device__ __forceinline__ void bm_locator(const uint8_t *__restrict__ ex,
+                                           const uint16_t *__restrict__ lg, const uint32_t *Sw,
+                                           int t, uint32_t (&C)[TMAX + 1], int &Lout) {
+    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL;
     int lS[2 * TMAX];  // lS[j-1] = log S_j
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) lS[2 * j] = lg[(Sw[j >> 2] >> (8 * (j & 3))) & 0xFFu];
@@ -114,7 +114,6 @@ __device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
         lS[e - 1] = (h == ZL) ? ZL : sq;
     }
     // inversionless binary Berlekamp-Massey over S_1, S_3, ... (even steps vanish)
-    uint32_t C[TMAX + 1];
     int lB[TMAX + 1];
 #pragma unroll
     for (int i = 0; i <= TMAX; ++i) { C[i] = i ? 0u : 1u; lB[i] = i ? ZL : 0; }
@@ -154,6 +153,19 @@ __device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
             lgam = chg ? ld : lgam;
         }
     }
+    Lout = L;
+}
+
+template <int M, int TMAX>
+__device__ __forceinline__ bool alg_core(const uint8_t *__restrict__ ex,
+                                         const uint16_t *__restrict__ lg,
+                                         const uint64_t *__restrict__ chien,
+                                         const uint32_t *Sw, int t,
+                                         Mask<Geo<M>::NW> &E) {
+    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL, NW = Geo<M>::NW;
+    uint32_t C[TMAX + 1];
+    int L;
+    bm_locator<M, TMAX>(ex, lg, Sw, t, C, L);
     int deg = 0;
 #pragma unroll
     for (int i = 1; i <= TMAX; ++i) deg = C[i] ? i : deg;
@@ -373,6 +385,98 @@ __device__ __forceinline__ bool alg_decode_word(const uint8_t *ex, const uint16_
     else
 #endif
         return alg_core<M, TMAX>(ex, lg, chien, Sw, t, E);
+}
+
+// Decoder::decode of ONE test word by a whole wave (its syndromes Sw wave-uniform): the
+// same decision and flipped positions as alg_core. Long codes (m >= 7) only, where one
+// lane's decode costs ~(t + 1)(n + 4t) table lookups and the LDS pipe, shared by the CU's
+// four SIMDs, is the bottleneck:
+//   * Berlekamp-Massey with lane i holding coefficient i of C (and B): per step one log
+//     lookup, one product per lane for the discrepancy -- summed by M ballot parities, no
+//     LDS -- and two products per lane for the update; the exact recurrence of bm_locator.
+//   * the Chien search of Decoder::locatorsAndRoots (:279-296) spread over the lanes: lane
+//     l tests the points of positions p = l + 64 s (root alpha^k flips position
+//     (n - k) mod n, :287), the locator's logs broadcast from lanes 0..deg.
+template <int M>
+__device__ __forceinline__ uint32_t wave_xor_bits(uint32_t v) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int b = 0; b < M; ++b) r |= (uint32_t)(__popcll(ballot((v >> b) & 1u)) & 1) << b;
+    return r;
+}
+
+template <int M, int TMAX>
+__device__ __forceinline__ bool alg_decode_wave(const uint8_t *__restrict__ ex,
+                                                const uint16_t *__restrict__ lg,
+                                                const uint32_t *Sw, int t, int lane,
+                                                Mask<Geo<M>::NW> &E) {
+    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL, NW = Geo<M>::NW, W = (TMAX + 3) / 4;
+    static_assert(2 * TMAX <= 64, "one syndrome per lane");
+    // lane q: log S_{q+1}; S_{2^e o} = S_o^(2^e) from the odd syndrome S_o (byte (o-1)/2)
+    int lSq;
+    {
+        const int j1 = lane + 1;
+        const int e = __builtin_ctz(j1);
+        const int o = j1 >> e;
+        const int jb = (o - 1) >> 1;  // odd-syndrome index
+        uint32_t wv = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) wv = (w == (jb >> 2)) ? Sw[w] : wv;
+        const uint32_t so = jb < TMAX ? (wv >> (8 * (jb & 3))) & 0xFFu : 0u;
+        const int ls = lg[so];
+        lSq = ls == ZL ? ZL : (int)(((uint32_t)ls << e) % (uint32_t)N);
+    }
+    uint32_t C = lane == 0 ? 1u : 0u;  // coefficient `lane` of C
+    int lB = lane == 0 ? 0 : ZL;       // log of coefficient `lane` of B
+    int lgam = 0, L = 0;
+    for (int k = 0; k < t; ++k) {
+        const int r = 2 * k;
+        const int lC = lg[C];
+        const int top = 2 * k - 1 > 0 ? (2 * k - 1 < TMAX ? 2 * k - 1 : TMAX) : 0;
+        const int lsv = __shfl(lSq, (r - lane) & 63, 64);  // log S_{r - lane + 1}
+        const uint32_t term = lane <= top ? gf_exp2<M>(ex, lC, lsv) : 0u;
+        const uint32_t d = uni((int)wave_xor_bits<M>(term));
+        const int ld = lg[d];
+        const bool chg = (d != 0u) && (2 * L <= r);
+        const int lBm1 = __shfl(lB, (lane - 1) & 63, 64);  // B_{lane-1}
+        const int lBm2 = __shfl(lB, (lane - 2) & 63, 64);
+        const int lCm1 = __shfl(lC, (lane - 1) & 63, 64);
+        const uint32_t g = gf_exp2<M>(ex, lgam, lC);
+        const uint32_t Cn = lane ? (g ^ gf_exp2<M>(ex, ld, lBm1)) : g;
+        C = (lane > 2 * k + 1 || lane > TMAX) ? 0u : Cn;
+        // B <- C_old (length change) or x B, then x B for the vanishing odd step
+        lB = lane == 0 ? ZL : (chg ? lCm1 : (lane >= 2 ? lBm2 : ZL));
+        L = chg ? r + 1 - L : L;
+        lgam = chg ? ld : lgam;
+    }
+    const uint64_t nz = ballot(C != 0u && lane <= TMAX) & ~1ull;
+    const int deg = nz ? 63 - (int)__builtin_clzll(nz) : 0;
+    const int ltl = lg[C];
+    int kk[NW], ik[NW];
+    uint32_t v[NW];
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const int pos = lane + 64 * s;
+        kk[s] = pos ? N - pos : 0;  // lambda(alpha^k) = sum_i C_i alpha^(i k)
+        ik[s] = 0;
+        v[s] = 0;
+    }
+    for (int i = 0; i <= deg; ++i) {  // wave-uniform trip count
+        const int lti = __builtin_amdgcn_readlane(ltl, i);
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            v[s] ^= gf_exp2<M>(ex, lti, ik[s]);  // log(0) clamps to exp = 0
+            ik[s] += kk[s];
+            ik[s] = ik[s] >= N ? ik[s] - N : ik[s];
+        }
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        E.w[s] = ballot(lane + 64 * s < N && v[s] == 0u);
+        cnt += __popcll(E.w[s]);
+    }
+    return (L <= t) && (deg >= 1) && (cnt == deg);
 }
 
 __device__ __forceinline__ void load_tables(uint8_t *dst, const uint8_t *src, uint32_t bytes) {

@@ -369,6 +369,7 @@ int fast_block_waves() { return kFastWaves; }
 
 // Fast-path instantiations (n <= 63, small t): (m, TMAX) as in select_kernels.
 bool select_fast(int m, int t, FastFn *out) {
+    if (m >= 7) return select_first_long(m, t, out);  // bchk_kernels.hip
 #define BCHK_FAST(MM, TT) \
     if (m == MM && t <= TT) { *out = &launch_fast_impl<MM, TT>; return true; }
     BCHK_FAST(3, 3)

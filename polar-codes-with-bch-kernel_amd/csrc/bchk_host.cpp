@@ -111,10 +111,12 @@ std::vector<uint8_t> make_generator(const Field &f, int t) {
     return g;
 }
 
-// Device table blob (see TableDesc in bchk_device.h).
-std::vector<uint8_t> make_tables(const Field &f, int t, TableDesc *td) {
+// Device table blob (see TableDesc in bchk_device.h). The syndrome columns are laid out
+// with the word count of the kernel instantiation (tmax, the TMAX bucket >= t): kernels
+// index them with a compile-time stride.
+std::vector<uint8_t> make_tables(const Field &f, int t, TableDesc *td, int tmax = 0) {
     const int n = f.n, m = f.m;
-    const int W = (std::max(t, 1) + 3) / 4;
+    const int W = (std::max(std::max(t, tmax), 1) + 3) / 4;
     const int EW = (m + 1) & ~1;
     auto align16 = [](size_t v) { return (v + 15) & ~size_t(15); };
     size_t off = 0;
@@ -591,7 +593,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
         delete c;
         return fail(BCHK_EINVAL, "no kernel instantiated for m=%d t=%d", m, t);
     }
-    c->tables_host = make_tables(c->field, t, &c->td);
+    c->tables_host = make_tables(c->field, t, &c->td, c->ks.tmax);
     int rc = 0;
     if (hipMalloc(&c->d_tables, c->td.bytes) != hipSuccess ||
         hipMemcpy(c->d_tables, c->tables_host.data(), c->td.bytes, hipMemcpyHostToDevice) != hipSuccess ||
@@ -605,7 +607,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     const size_t tb = (c->td.bytes + 15) & ~size_t(15);
     c->lds = tb + kWavesPerBlock * c->ks.wave_bytes;
     c->lds_alg = tb;
-    if (select_fast(m, t, &c->fast)) c->lds_fast = tb + fast_block_waves() * fast_wave_bytes();
+    if (select_fast(m, t, &c->fast))  // m >= 7: kaneko_first_kernel, the search kernel's layout
+        c->lds_fast = m >= 7 ? c->lds : tb + fast_block_waves() * fast_wave_bytes();
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     if (getenv("BCHK_NO_TABLE")) c->use_table = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);

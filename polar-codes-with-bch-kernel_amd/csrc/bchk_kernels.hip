@@ -45,6 +45,13 @@ struct Smem {
     static constexpr int WAVE_BYTES = NP * 8 * 2 + NP;
 };
 constexpr int kCoopWaves = 16;  // waves that share one heavy codeword (1024 threads)
+// long codes: test patterns decoded one at a time by the whole wave before the 64-pattern
+// chunks (search_codeword)
+#ifndef BCHK_SEQ_PATTERNS
+#define BCHK_SEQ_PATTERNS 4
+#endif
+constexpr int kSeqPatterns = BCHK_SEQ_PATTERNS;
+static_assert(kSeqPatterns >= 1 && kSeqPatterns <= 64, "sequential patterns lie in chunk 0");
 
 // ------------------------------------------------------- per-codeword prep
 // Reference: KanekoKernelProcessor::decode(answer, word, res) prologue and set-up,
@@ -65,10 +72,59 @@ struct Prep {
 };
 
 template <int M, int TMAX>
-__device__ void prep_codeword(const SearchParams &p, const uint32_t *col, double *as, double *ap,
+__device__ __forceinline__ void prep_syndromes(const uint32_t *col, int lane, Prep<M, TMAX> &P);
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Ascending bitonic sort of a wave's 64 NW keys, element e = lane + 64 s in key[s]:
+// partners at distance < 64 are exchanged across lanes, larger distances within a lane.
+template <int NW>
+__device__ __forceinline__ void wave_bitonic_sort(uint64_t (&key)[NW], int lane) {
+    constexpr int NE = 64 * NW;
+#pragma unroll
+    for (int kk = 2; kk <= NE; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+                const int js = j >> 6;
+#pragma unroll
+                for (int s = 0; s < NW; ++s) {
+                    if (s & js) continue;  // s is the lower element of the pair (s, s | js)
+                    const bool up = ((64 * s) & kk) == 0;
+                    const uint64_t a = key[s], b = key[s | js];
+                    const bool sw = up ? (a > b) : (a < b);
+                    key[s] = sw ? b : a;
+                    key[s | js] = sw ? a : b;
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < NW; ++s) {
+                    const int e = lane + 64 * s;
+                    const uint64_t o = shfl_xor64(key[s], j);
+                    const bool up = (e & kk) == 0;
+                    const bool lower = (lane & j) == 0;
+                    const bool takemin = lower == up;
+                    const bool lt = o < key[s];
+                    key[s] = (takemin == lt) ? o : key[s];
+                }
+            }
+        }
+    }
+}
+
+template <int M, int TMAX>
+__device__ __forceinline__ void prep_codeword(const SearchParams &p, const uint32_t *col, double *as, double *ap,
                               uint8_t *ordl, uint32_t cw, int lane, Prep<M, TMAX> &P) {
-    constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
-    constexpr int NB = N < 31 ? N : 31;  // pattern bits in use (i < 2^31)
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
     const double *y = p.y + (size_t)cw * N;
     // alpha = 2*word/pow(sd,2); yH; |alpha| (:336-342)
 #pragma unroll
@@ -81,14 +137,52 @@ __device__ void prep_codeword(const SearchParams &p, const uint32_t *col, double
         P.yH.w[s] = ballot(valid && !(al <= 0.0));
     }
     // exact rank by (|alpha|, position): the stable order of std::sort's keys (:343).
-    // |alpha| by position goes to LDS first; every lane then streams all N values with
-    // broadcast reads (uniform address, no bank conflict) and counts those ranked before it.
+    // |alpha| by position goes to LDS first.
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         const int pos = lane + 64 * s;
         if (pos < N) ap[pos] = P.av[s];
     }
     wave_sync();
+    if constexpr (M >= 7) {
+        // long codes: sort the wave's 64 NW keys (f64 bits of |alpha| with the low 8
+        // mantissa bits replaced by the position) with a bitonic network. Keys whose 55-bit
+        // |alpha| prefixes all differ are ordered exactly as (|alpha|, position); a prefix tie
+        // between sorted neighbours -- an exact tie or a near one -- takes the exact rank below.
+        uint64_t key[NW];
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            const int pos = lane + 64 * s;
+            key[s] = pos < N ? (((uint64_t)__double_as_longlong(P.av[s]) & ~0xFFull) | (uint64_t)pos)
+                             : ~0ull;
+        }
+        wave_bitonic_sort<NW>(key, lane);
+        bool ptie = false;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            uint64_t nx = shfl64(key[s], (lane + 1) & 63);
+            if (s + 1 < NW) nx = lane == 63 ? rdl64(key[s + 1 < NW ? s + 1 : s], 0) : nx;
+            const int e = lane + 64 * s;
+            ptie |= e + 1 < N && (key[s] >> 8) == (nx >> 8);
+        }
+        if (ballot(ptie) == 0ull) {
+#pragma unroll
+            for (int s = 0; s < NW; ++s) {
+                const int q = lane + 64 * s;
+                const int pos = (int)(key[s] & 0xFFull);
+                P.ordv[s] = q < N ? pos : 0;
+                P.asv[s] = q < N ? ap[pos] : 0.0;
+                if (q < N) {
+                    as[q] = P.asv[s];
+                    ordl[q] = (uint8_t)pos;
+                }
+            }
+            P.tie = false;
+            wave_sync();
+            prep_syndromes<M, TMAX>(col, lane, P);
+            return;
+        }
+    }
     int rk[NW];
     bool tie = false;
 #pragma unroll
@@ -121,6 +215,15 @@ __device__ void prep_codeword(const SearchParams &p, const uint32_t *col, double
         P.asv[s] = q < N ? as[q] : 0.0;
         P.ordv[s] = q < N ? ordl[q] : 0;
     }
+    prep_syndromes<M, TMAX>(col, lane, P);
+}
+
+// The hard decision's syndromes and the test-pattern syndrome columns (the prep's tail,
+// after the order is known).
+template <int M, int TMAX>
+__device__ __forceinline__ void prep_syndromes(const uint32_t *col, int lane, Prep<M, TMAX> &P) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
+    constexpr int NB = N < 31 ? N : 31;  // pattern bits in use (i < 2^31)
     // syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
 #pragma unroll
     for (int w = 0; w < W; ++w) P.S0[w] = 0;
@@ -274,7 +377,7 @@ __device__ __forceinline__ void init_state(SearchState<Geo<M>::NW> &S, int varia
 // loop after `success` (:372-398). Wave-uniform inputs; the calcT scan is lane-parallel.
 // Sets S.done when the reference loop would end after this iteration.
 template <int M, int TMAX>
-__device__ void accept_success(SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
+__device__ __forceinline__ void accept_success(SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
                                const Mask<Geo<M>::NW> &d, int m, double l, uint64_t ii,
                                const double *as, const SearchParams &p, int lane) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
@@ -347,7 +450,7 @@ __device__ void accept_success(SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &
 }
 
 template <int M, int TMAX>
-__device__ void write_outputs(const SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
+__device__ __forceinline__ void write_outputs(const SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
                               const SearchParams &p, uint32_t cw, int lane) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
     const bool word_variant = p.variant == BCHK_VARIANT_WORD;
@@ -381,6 +484,46 @@ __device__ void write_outputs(const SearchState<Geo<M>::NW> &S, const Prep<M, TM
     }
 }
 
+// Long codes: the first kSeqPatterns test patterns (the hard decision, :363-379, then
+// single flips of the least reliable positions -- at high SNR the hard decision is often a
+// codeword already, which Decoder::decode rejects) are decoded one at a time by the whole
+// wave, and most codewords leave the reference loop among them through
+// `l < calcRightSide()` (:380-382) without decoding a 64-pattern chunk. Otherwise the chunk
+// at base 0 decodes these patterns again to the same results; none of them is an
+// improvement a second time (l0 <= their l), so the state advances exactly as in the
+// reference. Sets S.done when the codeword's search has ended.
+template <int M, int TMAX>
+__device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
+                                               const SearchParams &p, const uint8_t *ex,
+                                               const uint16_t *lg, const double *as,
+                                               const double *ap, int lane) {
+    constexpr int NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
+    for (int i = 0; i < kSeqPatterns; ++i) {
+        if ((uint64_t)i >= S.bound) {  // the loop ends at its bound (:361)
+            S.i_end = S.bound;
+            S.done = true;
+            return;
+        }
+        uint32_t Sw[W];  // pattern i < 64: flips Plo of lane i, syndrome S0 ^ Lo of lane i
+#pragma unroll
+        for (int w = 0; w < W; ++w) Sw[w] = P.S0[w] ^ rdl(P.Lo[w], i);
+        Mask<NW> E;
+        const bool ok = alg_decode_wave<M, TMAX>(ex, lg, Sw, p.t, lane, E);
+        if (i == 0 && !ok) S.firstOK = false;  // :371
+        if (ok) {
+#pragma unroll
+            for (int s = 0; s < NW; ++s) E.w[s] ^= rdl64(P.Plo.w[s], i);  // yH ^ x
+            double l = 0.0;  // calcL (:69-77) in index order
+#pragma unroll
+            for (int s = 0; s < NW; ++s)
+                for (uint64_t v = E.w[s]; v; v &= v - 1) l += ap[64 * s + (int)__builtin_ctzll(v)];
+            if (l < S.l0) accept_success<M, TMAX>(S, P, E, mask_popc<NW>(E), l, (uint64_t)i, as, p, lane);
+            else if (i == 0 || !S.firstOK) S.m0 = mask_popc<NW>(E);  // :374 without improvement
+        }
+        if (S.done) return;
+    }
+}
+
 // ------------------------------------------------ wave-per-codeword search
 // 64 consecutive test patterns per step, acceptance in pattern order. A codeword still
 // running after p.chunk_limit steps is handed to the cooperative kernel (heavy queue).
@@ -393,6 +536,17 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
     SearchState<NW> S;
     init_state<M>(S, p.variant);
+    if constexpr (M >= 7) {
+        // long codes: the first test patterns one at a time, unless kaneko_first_kernel has
+        // done so already (it queued this codeword)
+        if (!p.queue) {
+            first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
+            if (S.done) {
+                write_outputs<M, TMAX>(S, P, p, cw, lane);
+                return;
+            }
+        }
+    }
     constexpr int G = chunk_group<TAB>();
     uint32_t chunks = 0;
     for (uint64_t base0 = 0;; base0 += 64 * G) {
@@ -523,6 +677,42 @@ kaneko_search_kernel(SearchParams p) {
         ++ndone;
     }
     wave_done(p, lane, ndone);
+}
+
+// --------------------------------------- long codes: first patterns of every codeword
+// The counterpart of the n <= 63 fast path (bchk_fast.hip) for m >= 7: one wave per
+// codeword, grid-stride over the batch, with only the prep and first_patterns in the
+// kernel, so it holds fewer registers than the search kernel and keeps more waves in flight
+// to hide the channel loads. A codeword whose search has not ended goes to the exact
+// kernel's queue (one atomic per queued codeword), which starts it from scratch.
+template <int M, int TMAX>
+__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock)
+kaneko_first_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    load_tables(smem, p.tables, p.td.bytes);
+    __syncthreads();
+    const uint8_t *ex = smem + p.td.off_exp;
+    const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
+    const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int NP = Smem<M, TMAX>::NP, NW = Geo<M>::NW;
+    uint8_t *wbase = smem + ((p.td.bytes + 15) & ~15u) + wid * Smem<M, TMAX>::WAVE_BYTES;
+    double *as = reinterpret_cast<double *>(wbase);
+    double *ap = as + NP;
+    uint8_t *ordl = wbase + NP * 16;
+    const uint32_t stride = gridDim.x * kWavesPerBlock;
+    for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride) {
+        Prep<M, TMAX> P;
+        prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+        SearchState<NW> S;
+        init_state<M>(S, p.variant);
+        first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
+        if (S.done) {
+            write_outputs<M, TMAX>(S, P, p, cw, lane);
+        } else if (lane == 0) {
+            p.queue_out[atomicAdd(p.qtail, 1u)] = cw;
+        }
+    }
 }
 
 // ---------------------------------------- cooperative search of heavy codewords
@@ -969,6 +1159,27 @@ template <int M, int TMAX, bool TAB>
 static const void *search_fn() { return reinterpret_cast<const void *>(&kaneko_search_kernel<M, TMAX, TAB>); }
 template <int M, int TMAX, bool TAB>
 static const void *coop_fn() { return reinterpret_cast<const void *>(&kaneko_coop_kernel<M, TMAX, TAB>); }
+
+// codewords per wave of kaneko_first_kernel (grid-stride): amortises the table staging
+constexpr uint32_t kFirstPerWave = 8;
+template <int M, int TMAX>
+static hipError_t launch_first_impl(const SearchParams &p, size_t lds, hipStream_t s) {
+    const uint32_t per_block = kWavesPerBlock * kFirstPerWave;
+    const int blocks = (int)((p.count + per_block - 1) / per_block);
+    hipLaunchKernelGGL((kaneko_first_kernel<M, TMAX>), dim3(blocks > 0 ? blocks : 1),
+                       dim3(kWaveSize * kWavesPerBlock), lds, s, p);
+    return hipGetLastError();
+}
+
+// Long-code first-pattern kernels (m >= 7), same (m, TMAX) buckets as select_kernels.
+bool select_first_long(int m, int t, FastFn *out) {
+#define BCHK_FIRST(MM, TT) \
+    if (m == MM && t <= TT) { *out = &launch_first_impl<MM, TT>; return true; }
+    BCHK_FIRST(7, 8) BCHK_FIRST(7, 16) BCHK_FIRST(7, 32)
+    BCHK_FIRST(8, 15) BCHK_FIRST(8, 16) BCHK_FIRST(8, 32)
+#undef BCHK_FIRST
+    return false;
+}
 
 template <int M, int TMAX>
 static KernelSet make_set() {

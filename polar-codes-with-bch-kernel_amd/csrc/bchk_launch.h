@@ -25,8 +25,10 @@ struct KernelSet {
 
 typedef hipError_t (*FastFn)(const SearchParams &, size_t, hipStream_t);
 
-// Lane-per-codeword fast path (bchk_fast.hip); false when (m, t) has none (n > 63, large t).
+// Fast path: lane per codeword for n <= 63 (bchk_fast.hip), first test patterns of every
+// codeword for m >= 7 (kaneko_first_kernel, bchk_kernels.hip); false when (m, t) has none.
 bool select_fast(int m, int t, FastFn *out);
+bool select_first_long(int m, int t, FastFn *out);
 size_t fast_wave_bytes();
 int fast_block_waves();  // waves per block of the fast kernel
 

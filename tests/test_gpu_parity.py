@@ -125,7 +125,10 @@ def test_word_variant_infile_known_answer():
 @pytest.mark.parametrize("exec_path", list(PATHS))
 @pytest.mark.parametrize("m,t,snr,B", [(6, 6, 3.0, 64), (6, 6, 4.0, 256), (6, 6, 5.0, 512),
                                        (6, 6, 6.0, 2048), (5, 3, 1.0, 256), (5, 3, 5.0, 2048),
-                                       (4, 2, 0.0, 512), (4, 2, 6.0, 2048), (8, 15, 5.0, 32)])
+                                       (4, 2, 0.0, 512), (4, 2, 6.0, 2048), (8, 15, 5.0, 32),
+                                       (8, 15, 6.0, 512), (8, 15, 7.0, 1024), (8, 4, 4.0, 128),
+                                       (7, 10, 5.0, 256), (7, 10, 6.5, 1024), (7, 3, 3.0, 256),
+                                       (6, 4, 4.0, 256), (4, 3, 3.0, 256), (5, 5, 3.0, 256)])
 def test_kaneko_j15_matches_oracle(m, t, snr, B, exec_path):
     o = Oracle(m, t)
     _, y = o.stream(101, B, snr)
@@ -319,3 +322,53 @@ def test_uncapped_batch_all_paths_agree_and_match_oracle():
     r2, l2, s2, a2 = o.kaneko_batch(y[rows], J=-1)
     res, l0, st = ref[0][rows], ref[1][rows], ref[2][rows]
     check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, res, l0, st)
+
+
+@pytest.mark.parametrize("m,t", [(8, 15), (7, 10)])
+def test_long_code_sort_and_first_pattern_edge_rows(m, t):
+    # long codes (m >= 7) order |alpha| with a bitonic sort of 55-bit prefixes and decode
+    # test pattern 0 with the whole wave: rows built to hit both -- exact |y| ties, ties
+    # of the prefix only (differ in the low mantissa bits), tiny / huge / zero samples,
+    # a noiseless codeword -- all equal to the oracle (tied rows flagged, as at n <= 63)
+    o = Oracle(m, t)
+    n = (1 << m) - 1
+    tx, y = o.stream(303, 64, 6.0)
+    y = y.copy()
+    y[0, 5] = -y[0, 9]                            # exact tie
+    y[1, 3] = np.nextafter(y[1, 8], np.inf if y[1, 8] > 0 else -np.inf)  # prefix tie, 1 ulp
+    y[2, 7] = 1e-300                              # subnormal |alpha| range
+    y[3, 7] = 1e300                               # huge
+    y[4, 11] = 0.0
+    y[5, :] = np.where(tx[5] == 1, 1.0, -1.0)     # noiseless codeword: all |y| tied
+    y[6, n - 1] = -y[6, 0] * (1 + 2.0 ** -50)     # prefix tie at the ends of the order
+    F = load()
+    for J in (15, -1):
+        for path in ("fast+exact+coop", "exact-only", "coop-heavy"):
+            d = dec(m, t, J=J, path=path)
+            d.set_max_decodes(1 << 16)
+            res, l0, st = d.decode(y)
+            d.set_max_decodes(0)
+            keep = (st["flags"] & (F.F_TIE | F.F_TRUNCATED)) == 0
+            assert st["flags"][0] & F.F_TIE and st["flags"][5] & F.F_TIE
+            assert keep[1] and keep[6]
+            r2, l2, s2, a2 = o.kaneko_batch(y[keep], J=J)
+            check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, res[keep], l0[keep], st[keep])
+
+
+def test_long_code_batch_paths_agree_and_sample_matches_oracle():
+    # BCH(255,139,31) at a batch large enough to fill the chip: all execution paths agree,
+    # and a sample matches the oracle (uncapped loop, the shipped semantics)
+    o = Oracle(8, 15)
+    ds = [dec(8, 15, J=-1, path=p) for p in ("fast+exact+coop", "exact-only", "coop-heavy")]
+    _, y, _ = ds[0].generate(6.5, 1 << 15, seed=41)
+    a = ds[0].decode(y)
+    for d in ds[1:]:
+        b = d.decode(y)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+        np.testing.assert_array_equal(a[2], b[2])
+    # (the sample skips the rare rows of > 5000 decodes, which take the CPU oracle minutes)
+    light = np.flatnonzero(a[2]["decodes"] < 5000)
+    idx = np.random.default_rng(3).choice(light, 200, replace=False)
+    r2, l2, s2, a2 = o.kaneko_batch(y[idx], J=-1)
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, a[0][idx], a[1][idx], a[2][idx])
