@@ -55,9 +55,44 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// v from lane ^ J, without the LDS crossbar: DPP quad permutes (J = 1, 2), row rotates
+// (J = 4: by 12 or 4 as bit 2 of the lane says; J = 8: by 8), and the gfx950 row/half swaps
+// v_permlane16_swap / v_permlane32_swap (J = 16, 32).
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v, int lane) {
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    } else if constexpr (J == 4) {
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12C, 0xF, 0xF, false);
+        return (lane & 4) ? dn : up;  // row_ror:4 reads lane - 4, row_ror:12 lane + 4
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+    } else if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else {
+        static_assert(J == 32, "lane distance");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    }
+}
+template <int J>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t v, int lane) {
+    return ((uint64_t)lane_xor<J>((uint32_t)(v >> 32), lane) << 32) | lane_xor<J>((uint32_t)v, lane);
+}
+
+// XOR over the wave
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
+    const int lane = (int)__lane_id();
+    v ^= lane_xor<32>(v, lane);
+    v ^= lane_xor<16>(v, lane);
+    v ^= lane_xor<8>(v, lane);
+    v ^= lane_xor<4>(v, lane);
+    v ^= lane_xor<2>(v, lane);
+    v ^= lane_xor<1>(v, lane);
     return v;
 }
 
@@ -80,8 +115,8 @@ __device__ __forceinline__ uint32_t gf_exp2(const uint8_t *ex, int la, int lb) {
 template <int NW>
 __device__ __forceinline__ void mask_set(Mask<NW> &m, int p) {
 #pragma unroll
-    for (int s = 0; s < NW; ++s)
-        if (s == (p >> 6)) m.w[s] |= 1ull << (p & 63);
+    for (int s = 0; s < NW; ++s)  // branch-free: a guarded store becomes a runtime index
+        m.w[s] |= (uint64_t)((p >> 6) == s) << (p & 63);
 }
 template <int NW>
 __device__ __forceinline__ int mask_popc(const Mask<NW> &m) {

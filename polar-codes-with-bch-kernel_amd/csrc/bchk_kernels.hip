@@ -79,59 +79,87 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
     return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-    return ((uint64_t)hi << 32) | lo;
+
+// One compare-exchange step of the bitonic network at lane distance J < 64.
+template <int J, int NW>
+__device__ __forceinline__ void bitonic_lane_step(uint64_t (&key)[NW], int kk, int lane) {
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const int e = lane + 64 * s;
+        const uint64_t o = lane_xor64<J>(key[s], lane);
+        const bool takemin = ((lane & J) == 0) == ((e & kk) == 0);
+        const bool lt = o < key[s];
+        key[s] = (takemin == lt) ? o : key[s];
+    }
 }
 
 // Ascending bitonic sort of a wave's 64 NW keys, element e = lane + 64 s in key[s]:
 // partners at distance < 64 are exchanged across lanes, larger distances within a lane.
+// Unrolled by template recursion, so every register index is a constant (a runtime index
+// would put the keys in scratch memory).
+template <int KK, int J, int NW>
+__device__ __forceinline__ void bitonic_merge_steps(uint64_t (&key)[NW], int lane) {
+    if constexpr (J >= 64) {
+        constexpr int js = J >> 6;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            if (s & js) continue;  // s is the lower element of the pair (s, s | js)
+            const bool up = ((64 * s) & KK) == 0;
+            const uint64_t a = key[s], b = key[s | js];
+            const bool sw = up ? (a > b) : (a < b);
+            key[s] = sw ? b : a;
+            key[s | js] = sw ? a : b;
+        }
+    } else {
+        bitonic_lane_step<J, NW>(key, KK, lane);
+    }
+    if constexpr (J > 1) bitonic_merge_steps<KK, J / 2, NW>(key, lane);
+}
+template <int KK, int NW>
+__device__ __forceinline__ void bitonic_stages(uint64_t (&key)[NW], int lane) {
+    bitonic_merge_steps<KK, KK / 2, NW>(key, lane);
+    if constexpr (KK < 64 * NW) bitonic_stages<2 * KK, NW>(key, lane);
+}
 template <int NW>
 __device__ __forceinline__ void wave_bitonic_sort(uint64_t (&key)[NW], int lane) {
-    constexpr int NE = 64 * NW;
-#pragma unroll
-    for (int kk = 2; kk <= NE; kk <<= 1) {
-#pragma unroll
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-            if (j >= 64) {
-                const int js = j >> 6;
-#pragma unroll
-                for (int s = 0; s < NW; ++s) {
-                    if (s & js) continue;  // s is the lower element of the pair (s, s | js)
-                    const bool up = ((64 * s) & kk) == 0;
-                    const uint64_t a = key[s], b = key[s | js];
-                    const bool sw = up ? (a > b) : (a < b);
-                    key[s] = sw ? b : a;
-                    key[s | js] = sw ? a : b;
-                }
-            } else {
-#pragma unroll
-                for (int s = 0; s < NW; ++s) {
-                    const int e = lane + 64 * s;
-                    const uint64_t o = shfl_xor64(key[s], j);
-                    const bool up = (e & kk) == 0;
-                    const bool lower = (lane & j) == 0;
-                    const bool takemin = lower == up;
-                    const bool lt = o < key[s];
-                    key[s] = (takemin == lt) ? o : key[s];
-                }
-            }
-        }
-    }
+    bitonic_stages<2, NW>(key, lane);
 }
+
+// the channel samples of codeword cw: yv[s] = position lane + 64 s (0 past n)
+template <int M>
+__device__ __forceinline__ void load_row(const SearchParams &p, uint32_t cw, int lane,
+                                         double (&yv)[Geo<M>::NW]) {
+    constexpr int N = Geo<M>::N;
+    const double *y = p.y + (size_t)cw * N;
+#pragma unroll
+    for (int s = 0; s < Geo<M>::NW; ++s) yv[s] = lane + 64 * s < N ? y[lane + 64 * s] : 0.0;
+}
+
+// prep from a row already loaded (yv[s] = sample of position lane + 64 s)
+template <int M, int TMAX>
+__device__ __forceinline__ void prep_loaded(const SearchParams &p, const uint32_t *col, double *as,
+                                            double *ap, uint8_t *ordl, const double (&yv)[Geo<M>::NW],
+                                            int lane, Prep<M, TMAX> &P);
 
 template <int M, int TMAX>
 __device__ __forceinline__ void prep_codeword(const SearchParams &p, const uint32_t *col, double *as, double *ap,
                               uint8_t *ordl, uint32_t cw, int lane, Prep<M, TMAX> &P) {
+    double yv[Geo<M>::NW];
+    load_row<M>(p, cw, lane, yv);
+    prep_loaded<M, TMAX>(p, col, as, ap, ordl, yv, lane, P);
+}
+
+template <int M, int TMAX>
+__device__ __forceinline__ void prep_loaded(const SearchParams &p, const uint32_t *col, double *as,
+                                            double *ap, uint8_t *ordl, const double (&yv)[Geo<M>::NW],
+                                            int lane, Prep<M, TMAX> &P) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
-    const double *y = p.y + (size_t)cw * N;
     // alpha = 2*word/pow(sd,2); yH; |alpha| (:336-342)
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         const int pos = lane + 64 * s;
         const bool valid = pos < N;
-        const double yy = valid ? y[pos] : 0.0;
+        const double yy = yv[s];
         const double al = (2.0 * yy) / p.s2;
         P.av[s] = valid ? fabs(al) : 0.0;
         P.yH.w[s] = ballot(valid && !(al <= 0.0));
@@ -686,7 +714,7 @@ kaneko_search_kernel(SearchParams p) {
 // to hide the channel loads. A codeword whose search has not ended goes to the exact
 // kernel's queue (one atomic per queued codeword), which starts it from scratch.
 template <int M, int TMAX>
-__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock)
+__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4)))
 kaneko_first_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
@@ -701,9 +729,34 @@ kaneko_first_kernel(SearchParams p) {
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
     const uint32_t stride = gridDim.x * kWavesPerBlock;
-    for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride) {
+    // the next codeword's row is loaded while this one is decoded (its latency hidden)
+    double ynext[NW];
+    uint32_t cw = blockIdx.x * kWavesPerBlock + wid;
+    if (cw < p.count) load_row<M>(p, cw, lane, ynext);
+    for (; cw < p.count; cw += stride) {
+        double yv[NW];
+#pragma unroll
+        for (int s = 0; s < NW; ++s) yv[s] = ynext[s];
+        if (cw + stride < p.count) load_row<M>(p, cw + stride, lane, ynext);
+#if defined(BCHK_FIRST_CUT) && BCHK_FIRST_CUT == 1
+        // experiment builds only (wrong results, timing of the phases): channel loads
+        if (yv[0] + yv[NW - 1] == 12345.0) p.l0[cw] = 0.0;  // keeps the loads
+        continue;
+#endif
         Prep<M, TMAX> P;
-        prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+        prep_loaded<M, TMAX>(p, col, as, ap, ordl, yv, lane, P);
+#if defined(BCHK_FIRST_CUT) && BCHK_FIRST_CUT == 2
+        ap[lane] = P.asv[0] + (double)P.S0[0] + (double)P.Lo[0];  // + prep (sort, syndromes)
+        continue;
+#endif
+#if defined(BCHK_FIRST_CUT) && BCHK_FIRST_CUT == 3
+        {  // + one wave decode
+            Mask<NW> E;
+            const bool ok = alg_decode_wave<M, TMAX>(ex, lg, P.S0, p.t, lane, E);
+            ap[lane] = P.asv[0] + (ok ? (double)E.w[0] : 0.0);
+        }
+        continue;
+#endif
         SearchState<NW> S;
         init_state<M>(S, p.variant);
         first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
