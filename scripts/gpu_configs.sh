@@ -16,3 +16,4 @@ for S in 5 6; do run --snr $S --J -1; done
 for S in 0 2 4 6; do run --m 5 --t 3 --batch 262144 --snr $S --J 15 --steps 5; done
 for S in 2 4 6; do run --m 5 --t 3 --batch 262144 --snr $S --J -1 --steps 5; done
 for S in 6 7; do run --m 8 --t 15 --snr $S --J -1 --steps 3 --warmup 1; done
+for S in 5 6 7; do run --m 8 --t 15 --snr $S --J 15 --steps 3 --warmup 1; done
