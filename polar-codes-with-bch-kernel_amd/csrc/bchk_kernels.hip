@@ -541,10 +541,12 @@ __device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const
         if (ok) {
 #pragma unroll
             for (int s = 0; s < NW; ++s) E.w[s] ^= rdl64(P.Plo.w[s], i);  // yH ^ x
-            double l = 0.0;  // calcL (:69-77) in index order
+            // calcL (:69-77) in index order; position lane + 64 s holds its |alpha| in
+            // P.av[s], so the terms come by readlane instead of dependent LDS loads
+            double l = 0.0;
 #pragma unroll
             for (int s = 0; s < NW; ++s)
-                for (uint64_t v = E.w[s]; v; v &= v - 1) l += ap[64 * s + (int)__builtin_ctzll(v)];
+                for (uint64_t v = E.w[s]; v; v &= v - 1) l += rdlf(P.av[s], (int)__builtin_ctzll(v));
             if (l < S.l0) accept_success<M, TMAX>(S, P, E, mask_popc<NW>(E), l, (uint64_t)i, as, p, lane);
             else if (i == 0 || !S.firstOK) S.m0 = mask_popc<NW>(E);  // :374 without improvement
         }
