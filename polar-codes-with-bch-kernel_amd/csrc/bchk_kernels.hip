@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <float.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include "bchk_core.h"
@@ -1285,7 +1286,12 @@ hipError_t launch_alg(const KernelSet &k, const AlgParams &p, size_t lds, hipStr
 }
 hipError_t launch_count(int n, const uint8_t *tx, const uint8_t *res, const bchk_stats *st,
                         uint32_t B, uint64_t *out6, hipStream_t s) {
-    const int grid = (int)((B + 255) / 256) < 16384 ? (int)((B + 255) / 256) : 16384;
+    // grid-stride: every block ends with 6 atomics on the same 6 words, so the grid is capped
+    // (1024 blocks: 43.6 us at 2^20 x 63 vs 67.8 us with one block per 256 rows,
+    // profiles/r01_long/count_grid.jsonl)
+    // (BCHK_COUNT_GRID overrides the cap for experiments)
+    static const int cap = getenv("BCHK_COUNT_GRID") ? atoi(getenv("BCHK_COUNT_GRID")) : 1024;
+    const int grid = (int)((B + 255) / 256) < cap ? (int)((B + 255) / 256) : cap;
     unsigned long long *o = reinterpret_cast<unsigned long long *>(out6);
     switch (n) {
 #define BCHK_CNT(NN) \
