@@ -133,11 +133,35 @@ void *bchk_stream(bchk_ctx *ctx);
  * number of decode calls, then resets. */
 int bchk_profile(bchk_ctx *ctx, int enable);
 int bchk_profile_read(bchk_ctx *ctx, double *ms3, uint64_t *launches);
+/* The same per stage: [0] fast, [1] exact first pass, [2] cooperative, [3] analytic tail
+ * kernel (bchk_set_analytic); bchk_profile_read's exact stage is [1] + [3]. */
+int bchk_profile_read_stages(bchk_ctx *ctx, double *ms4, uint64_t *launches);
 /* Codewords the last decode call handed from the fast path to the exact kernel, and from
  * the exact kernel to the cooperative kernel (synchronises the context's stream). */
 int bchk_path_counts(bchk_ctx *ctx, uint64_t *to_exact, uint64_t *to_coop);
+/* Codewords the last decode call's exact first pass handed to the analytic tail kernel. */
+int bchk_tail_count(bchk_ctx *ctx, uint64_t *to_tail);
+/* Outcomes of the last call's analytic tail: [0] handed on to the cooperative kernel,
+ * [1] finished from the candidate codewords, [2] split (exact chunks below the earliest
+ * candidate within the tightened bound, then the candidates), [3] exact chunks of [2],
+ * [4] enumeration steps (64 nodes each) summed, [5] their maximum over codewords. */
+int bchk_tail_stats(bchk_ctx *ctx, uint64_t *out6);
+/* Diagnostics (context created with BCHK_TAIL_DIAG=1 in the environment): the last call's
+ * per-codeword analytic-tail records, 8 u64 each -- codeword, cycles of prep, of the exact
+ * chunks, of the plan, enumeration steps, mode | reason << 8 | split chunks << 16, cycles
+ * after the plan, decodes. count = records written (may exceed items). */
+int bchk_tail_diag_read(bchk_ctx *ctx, uint64_t *out, size_t items, uint64_t *count);
 /* Enable (default) or disable the fast path; results are identical either way. */
 int bchk_set_fast_path(bchk_ctx *ctx, int enable);
+/* Enable (default) or disable the analytic tail of the exact kernel (n <= 63, decode
+ * variant): a codeword still searching after the chunk limit is finished from its candidate
+ * codewords -- those within t of some test pattern whose path metric can still improve
+ * (KanekoKernelProcessor.cpp:361-405 replayed over them) -- instead of decoding every test
+ * pattern in the cooperative kernel. Results are identical either way. */
+int bchk_set_analytic(bchk_ctx *ctx, int enable);
+/* 64-pattern chunks the exact kernel decodes before the analytic tail / the hand-off to
+ * the cooperative kernel (default 1; 0 = neither: the exact kernel decodes everything). */
+int bchk_set_chunk_limit(bchk_ctx *ctx, uint32_t chunks);
 
 /* Enable (default) or disable the syndrome decoding table of the search kernels: for
  * n <= 63 and m (t - 1) <= 30, Decoder::decode of a test pattern is a lookup of its

@@ -32,7 +32,9 @@ EXPORTS = (
     "bchk_set_max_decodes", "bchk_decode_host", "bchk_decode_device",
     "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device",
     "bchk_generate_host", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
-    "bchk_profile_read", "bchk_path_counts", "bchk_set_fast_path", "bchk_set_syndrome_table",
+    "bchk_profile_read", "bchk_profile_read_stages", "bchk_path_counts", "bchk_tail_count",
+    "bchk_tail_stats", "bchk_tail_diag_read", "bchk_set_fast_path", "bchk_set_analytic",
+    "bchk_set_chunk_limit", "bchk_set_syndrome_table",
     "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_polar_create",
     "bchk_polar_destroy", "bchk_polar_params", "bchk_polar_decode_host", "bchk_polar_decode_device",
     "bchk_polar_encode_host", "bchk_polar_sync", "bchk_polar_stream", "bchk_last_error", "bchk_version",
@@ -107,6 +109,12 @@ def lib():
     L.bchk_syndrome_table_info.argtypes = [i32, i32, C.POINTER(u64), C.POINTER(u64),
                                            C.POINTER(C.c_uint32)]
     L.bchk_path_counts.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)]
+    L.bchk_tail_count.argtypes = [vp, C.POINTER(u64)]
+    L.bchk_tail_stats.argtypes = [vp, C.POINTER(u64)]
+    L.bchk_tail_diag_read.argtypes = [vp, C.POINTER(u64), sz, C.POINTER(u64)]
+    L.bchk_profile_read_stages.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
+    L.bchk_set_analytic.argtypes = [vp, i32]
+    L.bchk_set_chunk_limit.argtypes = [vp, C.c_uint32]
     L.bchk_last_error.restype = C.c_char_p
     L.bchk_version.restype = C.c_char_p
     _lib = L
@@ -224,6 +232,43 @@ class KanekoKernelProcessor:
         n = C.c_uint64()
         _check(lib().bchk_profile_read(self._h, ms, C.byref(n)))
         return list(ms), n.value
+
+    def profile_read_stages(self):
+        """([fast, exact first pass, coop, analytic tail] kernel ms, decode calls)."""
+        ms = (C.c_double * 4)()
+        n = C.c_uint64()
+        _check(lib().bchk_profile_read_stages(self._h, ms, C.byref(n)))
+        return list(ms), n.value
+
+    def tail_count(self):
+        """Codewords the last call's first pass handed to the analytic tail kernel."""
+        a = C.c_uint64()
+        _check(lib().bchk_tail_count(self._h, C.byref(a)))
+        return a.value
+
+    def tail_stats(self):
+        """Last call's analytic tail outcomes: [handed on, finished, split, split chunks,
+        enumeration steps, max steps per codeword]."""
+        a = (C.c_uint64 * 6)()
+        _check(lib().bchk_tail_stats(self._h, a))
+        return list(a)
+
+    def tail_diag(self, items=65536):
+        """Diagnostics (context created with BCHK_TAIL_DIAG=1): per-codeword tail records."""
+        import numpy as np
+        out = np.zeros((items, 8), np.uint64)
+        n = C.c_uint64()
+        _check(lib().bchk_tail_diag_read(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), items,
+                                         C.byref(n)))
+        return out[:min(items, n.value)]
+
+    def set_analytic(self, enable=True):
+        """Analytic tail of heavy codewords (results identical either way)."""
+        _check(lib().bchk_set_analytic(self._h, 1 if enable else 0))
+
+    def set_chunk_limit(self, chunks):
+        """64-pattern chunks of the exact first pass before the tail / hand-off."""
+        _check(lib().bchk_set_chunk_limit(self._h, int(chunks)))
 
     def path_counts(self):
         """(codewords handed to the exact kernel, to the cooperative kernel) last call."""

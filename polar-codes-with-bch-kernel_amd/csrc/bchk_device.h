@@ -76,6 +76,19 @@ struct SearchParams {
     int32_t t;
     int32_t J;             // < 0: shipped
     int32_t variant;       // BCHK_VARIANT_*
+    // search kernel: after chunk_limit exact chunks, finish the codeword from its candidate
+    // codewords (bchk_kernels.hip, analytic tail) instead of handing it off; 0 = hand off
+    int32_t analytic;
+    // analytic tail outcomes (null = not counted): [0] handed on to the cooperative kernel,
+    // [1] finished from the candidates, [2] split (exact chunks, then the candidates),
+    // [3] exact chunks of the splits
+    uint32_t *tail_stats;
+    // diagnostics: per codeword through the analytic tail, 8 u64 (codeword, cycles of prep,
+    // exact chunks, plan, enumeration steps, mode | why << 8 | split chunks << 16, cycles
+    // after the plan, decodes); null = off
+    unsigned long long *tail_diag;
+    uint32_t *tail_diag_count;
+    uint32_t tail_diag_cap;
 };
 
 struct AlgParams {

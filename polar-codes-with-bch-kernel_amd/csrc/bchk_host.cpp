@@ -371,25 +371,31 @@ struct bchk_ctx {
     bool use_fast = true;
     size_t lds_fast = 0, lds_coop = 0;
     int grid_coop = 0, grid_coop_tab = 0;
-    uint32_t chunk_limit = 4;
+    uint32_t chunk_limit = 2;
     DevBuf queue, heavy, ctrl, diag;  // work queues + control words (one 128-B line each)
     uint8_t *d_tables = nullptr;
     hipStream_t stream = nullptr;
-    size_t lds = 0, lds_alg = 0;
-    int grid = 0, grid_tab = 0;
+    size_t lds = 0, lds_alg = 0, lds_tail = 0;
+    int grid = 0, grid_tab = 0, grid_tail = 0, grid_tail_tab = 0;
+    DevBuf l1q;  // first pass -> analytic tail kernel
     uint64_t max_decodes = 0;
     DevBuf y, res, l0, st, words, synd, ok;
     // the cooperative kernel runs on `aux`, concurrently with the exact kernel
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool coop_concurrent = false;  // BCHK_COOP_CONCURRENT=1: measured neutral at 5 dB
+    bool analytic = true;          // analytic tail of heavy codewords (BCHK_NO_ANALYTIC=1: off)
+    uint64_t last_tail = 0;        // codewords the last call handed to the tail kernel
+    uint64_t last_tail_stats[6] = {0, 0, 0, 0, 0, 0};
+    bool tail_diag_on = false;     // BCHK_TAIL_DIAG=1: per-codeword tail timing records
+    DevBuf tdiag;
     bool profile = false;
     // syndrome decoding table (bchk_syndtab.h): built on first use, shared across contexts
     bool use_table = true;
     SyndTable tab{};
-    struct Ev { hipEvent_t e[6]; };  // [fast, exact, coop] x [start, end] of one call
+    struct Ev { hipEvent_t e[8]; };  // [fast, exact, coop, tail] x [start, end] of one call
     std::vector<Ev> events;
-    double prof_ms[3] = {0.0, 0.0, 0.0};
+    double prof_ms[4] = {0.0, 0.0, 0.0, 0.0};
     uint64_t prof_launches = 0;
 };
 
@@ -404,11 +410,13 @@ int sigma_s2(int k, int n, double snr_db, double *sd) {
 
 // control block: fast-path queue tail (line 0), 8 per-XCD heads (lines 1-8), heavy front
 // tail / head (lines 9, 10), back tail / head (11, 12), 8 per-XCD counts of codewords the
-// exact kernel has finished (13-20), diagnostic record count (21); zeroed by one memset
-// per decode call
-constexpr size_t kCtrlBytes = 22 * 128;
+// exact kernel has finished (13-20), diagnostic record count (21), the first pass's
+// hand-offs to the analytic tail kernel (22), its 8 per-XCD heads (23-30) and finished
+// counts (31-38), its outcome counters (39); zeroed by one memset per decode call
+constexpr size_t kCtrlBytes = 40 * 128;
 constexpr int kHeavyTail = 32 * 9, kHeavyHead = 32 * 10, kHeavyTail2 = 32 * 11,
-              kHeavyHead2 = 32 * 12, kExactDone = 32 * 13;
+              kHeavyHead2 = 32 * 12, kExactDone = 32 * 13, kL1Tail = 32 * 22, kTailHeads = 32 * 23,
+              kTailDone = 32 * 31, kTailStats = 32 * 39;
 #ifdef BCHK_DIAG
 constexpr int kDiagCount = 32 * 21;
 #endif
@@ -487,6 +495,7 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     p.exact_total = fast ? ctrl : nullptr;  // the fast path's queue length
     p.heavy_big = kHeavyBig;
     p.chunk_limit = c->chunk_limit;
+    p.analytic = 0;
     if (c->use_table) p.tab = c->tab;
 #ifdef BCHK_DIAG
     if (!c->diag.p) (void)c->diag.ensure(size_t(1) << 24);
@@ -498,7 +507,11 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     const bool tabk = p.tab.slots && c->ks.search_tab;
     const int grid = tabk ? c->grid_tab : c->grid;
     const int grid_coop = tabk ? c->grid_coop_tab : c->grid_coop;
-    const bool conc = c->coop_concurrent && p.heavy_tail;
+    // analytic tail: the first pass hands its heavy codewords to the tail kernel (queue
+    // l1q), which finishes most of them and hands the rest to the cooperative kernel
+    const bool tail = c->analytic && c->ks.tail && p.heavy_tail && variant == BCHK_VARIANT_ANSWER;
+    if (tail && (rc = c->l1q.ensure(B * sizeof(uint32_t)))) return rc;
+    const bool conc = c->coop_concurrent && p.heavy_tail && !tail;
     hipStream_t cs = conc ? c->aux : s;  // the cooperative kernel's stream
     bchk_ctx::Ev ev{};
     if (c->profile) {
@@ -521,21 +534,50 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         HIP_TRY(hipStreamWaitEvent(cs, c->ev_fork, 0));
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[2], s));
-    if (fast) {
+    {
         SearchParams q = p;
-        q.queue = (const uint32_t *)c->queue.p;
-        q.qcount = ctrl;
-        q.heads = ctrl + 32;
-        // every resident wave may take work; waves beyond the queue length exit at once
-        HIP_TRY(launch_search(c->ks, q, grid, c->lds, s));
-    } else {
-        const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
-        HIP_TRY(launch_search(c->ks, p, std::max(1, std::min(grid, need)), c->lds, s));
+        if (tail) {  // hand-offs (all to the front) into the tail kernel's queue
+            q.heavy_queue = (uint32_t *)c->l1q.p;
+            q.heavy_tail = ctrl + kL1Tail;
+            q.heavy_big = 0;
+        }
+        if (fast) {
+            q.queue = (const uint32_t *)c->queue.p;
+            q.qcount = ctrl;
+            q.heads = ctrl + 32;
+            // every resident wave may take work; waves beyond the queue length exit at once
+            HIP_TRY(launch_search(c->ks, q, grid, c->lds, s));
+        } else {
+            const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
+            HIP_TRY(launch_search(c->ks, q, std::max(1, std::min(grid, need)), c->lds, s));
+        }
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[3], s));
+    SearchParams pc = p;  // the cooperative kernel's view of its producer
+    if (c->profile) HIP_TRY(hipEventRecord(ev.e[6], s));
+    if (tail) {
+        SearchParams q = p;
+        q.queue = (const uint32_t *)c->l1q.p;
+        q.qcount = ctrl + kL1Tail;
+        q.heads = ctrl + kTailHeads;
+        q.exact_done = ctrl + kTailDone;
+        q.analytic = 1;
+        q.tail_stats = ctrl + kTailStats;
+        if (c->tail_diag_on) {
+            if (!c->tdiag.p && (rc = c->tdiag.ensure(size_t(1) << 22))) return rc;
+            HIP_TRY(hipMemsetAsync(c->tdiag.p, 0, c->tdiag.cap, s));
+            q.tail_diag = (unsigned long long *)c->tdiag.p;
+            q.tail_diag_count = ctrl + kTailStats + 16;
+            q.tail_diag_cap = (uint32_t)(c->tdiag.cap / 64);
+        }
+        HIP_TRY(launch_tail(c->ks, q, tabk ? c->grid_tail_tab : c->grid_tail, c->lds_tail, s));
+        pc.exact_done = ctrl + kTailDone;
+        pc.exact_total = ctrl + kL1Tail;
+    }
+    if (c->profile) HIP_TRY(hipEventRecord(ev.e[7], s));
     if (p.heavy_tail) {
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));
-        HIP_TRY(launch_coop(c->ks, p, grid_coop, c->lds_coop, cs));
+        HIP_TRY(launch_coop(c->ks, pc, grid_coop, c->lds_coop, cs));
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[5], cs));
     } else if (c->profile) {
         HIP_TRY(hipEventRecord(ev.e[4], s));
@@ -606,6 +648,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     }
     const size_t tb = (c->td.bytes + 15) & ~size_t(15);
     c->lds = tb + kWavesPerBlock * c->ks.wave_bytes;
+    c->lds_tail = tb + kWavesPerBlock * c->ks.tail_wave_bytes;
     c->lds_alg = tb;
     if (select_fast(m, t, &c->fast))  // m >= 7: kaneko_first_kernel, the search kernel's layout
         c->lds_fast = m >= 7 ? c->lds : tb + fast_block_waves() * fast_wave_bytes();
@@ -613,6 +656,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (getenv("BCHK_NO_TABLE")) c->use_table = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);
     if (const char *cc = getenv("BCHK_COOP_CONCURRENT")) c->coop_concurrent = atoi(cc) != 0;
+    if (getenv("BCHK_NO_ANALYTIC")) c->analytic = false;
+    if (getenv("BCHK_TAIL_DIAG")) c->tail_diag_on = true;
     c->lds_coop = tb + c->ks.coop_bytes;
     // one cooperative workgroup per CU by default (LDS sized past half the CU's 160 KB):
     // a heavy codeword's 16 waves then own the CU's four SIMDs, which shortens the longest
@@ -637,6 +682,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
         c->grid_coop_tab = grid_of(c->ks.coop_tab_ptr(), kCoopThreads, c->lds_coop);
         c->grid_tab = grid_of(c->ks.search_tab_ptr(), kWaveSize * kWavesPerBlock, c->lds);
     }
+    if (c->ks.tail) c->grid_tail = grid_of(c->ks.tail_ptr(), kWaveSize * kWavesPerBlock, c->lds_tail);
+    if (c->ks.tail_tab) c->grid_tail_tab = grid_of(c->ks.tail_tab_ptr(), kWaveSize * kWavesPerBlock, c->lds_tail);
     (void)rc;
     *out = c;
     return 0;
@@ -647,6 +694,8 @@ void bchk_destroy(bchk_ctx *c) {
     for (auto &e : c->events)
         for (auto &x : e.e) (void)hipEventDestroy(x);
     c->queue.release();
+    c->l1q.release();
+    c->tdiag.release();
     c->heavy.release();
     c->ctrl.release();
     c->y.release();
@@ -890,12 +939,12 @@ int bchk_profile(bchk_ctx *c, int enable) {
     return 0;
 }
 
-int bchk_profile_read(bchk_ctx *c, double *ms3, uint64_t *launches) {
+int bchk_profile_read_stages(bchk_ctx *c, double *ms4, uint64_t *launches) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
     for (auto &e : c->events) {
         HIP_TRY(hipEventSynchronize(e.e[5]));
-        HIP_TRY(hipEventSynchronize(e.e[1]));
-        for (int k = 0; k < 3; ++k) {
+        HIP_TRY(hipEventSynchronize(e.e[7]));
+        for (int k = 0; k < 4; ++k) {
             float ms = 0.f;
             HIP_TRY(hipEventElapsedTime(&ms, e.e[2 * k], e.e[2 * k + 1]));
             c->prof_ms[k] += ms;
@@ -904,11 +953,51 @@ int bchk_profile_read(bchk_ctx *c, double *ms3, uint64_t *launches) {
         for (auto &x : e.e) (void)hipEventDestroy(x);
     }
     c->events.clear();
-    if (ms3)
-        for (int k = 0; k < 3; ++k) ms3[k] = c->prof_ms[k];
+    if (ms4)
+        for (int k = 0; k < 4; ++k) ms4[k] = c->prof_ms[k];
     if (launches) *launches = c->prof_launches;
-    c->prof_ms[0] = c->prof_ms[1] = c->prof_ms[2] = 0.0;
+    for (int k = 0; k < 4; ++k) c->prof_ms[k] = 0.0;
     c->prof_launches = 0;
+    return 0;
+}
+
+int bchk_profile_read(bchk_ctx *c, double *ms3, uint64_t *launches) {
+    double ms4[4];
+    if (int rc = bchk_profile_read_stages(c, ms4, launches)) return rc;
+    if (ms3) {  // the exact stage includes the analytic tail kernel
+        ms3[0] = ms4[0];
+        ms3[1] = ms4[1] + ms4[3];
+        ms3[2] = ms4[2];
+    }
+    return 0;
+}
+
+int bchk_tail_count(bchk_ctx *c, uint64_t *to_tail) {
+    if (!c || !to_tail) return fail(BCHK_EINVAL, "NULL argument");
+    uint64_t a = 0, b = 0;
+    if (int rc = bchk_path_counts(c, &a, &b)) return rc;
+    *to_tail = c->last_tail;
+    return 0;
+}
+
+// diagnostics (BCHK_TAIL_DIAG=1): the last call's per-codeword tail records, 8 u64 each
+int bchk_tail_diag_read(bchk_ctx *c, uint64_t *out, size_t items, uint64_t *count) {
+    if (!c || !out || !count) return fail(BCHK_EINVAL, "NULL argument");
+    *count = 0;
+    if (!c->tdiag.p) return 0;
+    uint32_t n = 0;
+    HIP_TRY(hipMemcpy(&n, (uint32_t *)c->ctrl.p + kTailStats + 16, 4, hipMemcpyDeviceToHost));
+    const size_t m = std::min<size_t>({items, (size_t)n, c->tdiag.cap / 64});
+    HIP_TRY(hipMemcpy(out, c->tdiag.p, m * 64, hipMemcpyDeviceToHost));
+    *count = n;
+    return 0;
+}
+
+int bchk_tail_stats(bchk_ctx *c, uint64_t *out6) {
+    if (!c || !out6) return fail(BCHK_EINVAL, "NULL argument");
+    uint64_t a = 0, b = 0;
+    if (int rc = bchk_path_counts(c, &a, &b)) return rc;
+    for (int k = 0; k < 6; ++k) out6[k] = c->last_tail_stats[k];
     return 0;
 }
 
@@ -921,6 +1010,8 @@ int bchk_path_counts(bchk_ctx *c, uint64_t *to_exact, uint64_t *to_coop) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         v[0] = h[0];
         v[1] = (uint64_t)h[kHeavyTail] + h[kHeavyTail2];
+        c->last_tail = h[kL1Tail];
+        for (int k = 0; k < 6; ++k) c->last_tail_stats[k] = h[kTailStats + k];
     }
     if (to_exact) *to_exact = v[0];
     if (to_coop) *to_coop = v[1];
@@ -983,6 +1074,18 @@ int bchk_syndrome_table_info(int m, int t, uint64_t *keys, uint64_t *bytes, uint
     if (keys) *keys = h->keys;
     if (bytes) *bytes = h->slots.size() * sizeof(uint64_t);
     if (max_probe) *max_probe = h->max_probe;
+    return 0;
+}
+
+int bchk_set_analytic(bchk_ctx *c, int enable) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    c->analytic = enable != 0;
+    return 0;
+}
+
+int bchk_set_chunk_limit(bchk_ctx *c, uint32_t chunks) {
+    if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    c->chunk_limit = chunks;
     return 0;
 }
 

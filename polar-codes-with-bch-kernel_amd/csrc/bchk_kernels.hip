@@ -555,18 +555,393 @@ __device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const
     }
 }
 
+// ------------------------------------------ analytic tail of the search (n <= 63)
+// Test pattern i flips the positions ord[b] of the set bits b of i, all among the NB least
+// reliable positions R (i < 2^NB). It succeeds exactly when some codeword c lies within
+// distance 1..t of yH ^ P_i (Decoder::decode, src/Decoder.cpp:298-321), and then yields c.
+// Write D = yH ^ c = D_U + D_R (U: the other positions). c is reached by some pattern iff
+// |D_U| <= t, and syn(D_R) = S0 ^ syn(D_U) (c is a codeword), i.e. S0 ^ syn(D_U) lies in the
+// span V of R's syndrome columns; D_R then follows from the column basis (plus the kernel
+// of R's columns). The first pattern that yields c is D_R with its t - |D_U| highest bits
+// cleared. Only first occurrences can improve l0 (a later one has the same l), and an
+// improvement needs l(c) < l0, where l(c) >= sum of a over D_U. So the rest of the
+// reference loop (src/KanekoKernelProcessor.cpp:361-405) is decided by the codewords whose
+// D_U has at most t elements and reliability sum below l0: a depth-first enumeration over U
+// in ascending reliability order, pruned at l0, finds all of them, and the reference's
+// acceptance logic is replayed over them in first-pattern order -- same result, same
+// counters, without decoding the thousands of test patterns in between.
+// When l0 is too loose for the node budget, the enumeration runs at a tighter bound lim
+// (the sum of the k least reliable U positions): the earliest candidate c* with
+// l(c*) <= lim at pattern i* splits the search -- patterns below i* are decoded exactly
+// (chunks, as before), and from i* on every improvement has l < l0 <= lim, so it is among
+// the enumerated candidates. Nothing fits (stack, candidate list, kernel dimension,
+// budget): the codeword is handed to the cooperative kernel as before.
+constexpr int kAnStack = 256;            // pending nodes of the enumeration
+constexpr int kAnCand = 64;              // candidate codewords kept for the replay
+constexpr int kAnKern = 3;               // kernel dimension of R's columns (2^3 combinations)
+constexpr uint32_t kAnBudget = 4096;     // enumeration nodes per attempt
+constexpr uint32_t kAnExactChunks = 32;  // exact chunks below the split pattern
+constexpr int kAnMaxU = 32;              // |U| <= 32 (n = 63 with NB = 31)
+
+struct AnNode {  // enumeration node: D_U = sel (bits over U indices)
+    uint64_t rem, pos;  // residual syndrome (zero: a codeword), D_U positions
+    int64_t sum;        // sum of a over D_U, fixed point (a lower bound)
+    uint32_t sel, comb; // U indices; pattern bits of D_R for this D_U
+};
+struct AnCand {
+    uint64_t D;  // yH ^ c (positions)
+    double l;    // calcL(c), index order
+    uint32_t i, m;
+};
+struct AnWave {
+    AnNode stack[kAnStack];
+    AnCand cand[kAnCand];
+    int64_t afix[kAnMaxU + 1];  // a of U index q, fixed point (2^40), sentinel at NU
+    uint64_t ru[kAnMaxU];
+    uint32_t cu[kAnMaxU];
+    uint32_t kern[kAnKern];
+    uint32_t ncand;
+    uint8_t pu[kAnMaxU];
+};
+template <int M, int TMAX>
+constexpr bool an_capable() { return Geo<M>::NW == 1 && TMAX <= 8; }
+template <int M, int TMAX>
+constexpr int an_bytes() { return an_capable<M, TMAX>() ? (int)((sizeof(AnWave) + 15) & ~size_t(15)) : 0; }
+
+// floor(a 2^40) (a lower bound of a in fixed point; huge values clamp low, still a bound)
+__device__ __forceinline__ int64_t an_fix(double a) {
+    return a < 0x1p17 ? (int64_t)(a * 0x1p40) : (int64_t)1 << 57;
+}
+// a fixed-point bound at least lim 2^40 (no pruning for huge bounds)
+__device__ __forceinline__ int64_t an_fix_up(double lim) {
+    return lim < 0x1p17 ? (int64_t)(lim * 0x1p40) + 1 : (int64_t)0x7FFFFFFFFFFFFFFFll;
+}
+
+// One enumerated codeword with residual zero: its D_R options (kernel combinations), first
+// pattern, filters (not yet processed exactly, below every possible bound, l < l0), and the
+// candidate list (per lane, divergent).
+template <int TMAX>
+__device__ __forceinline__ void an_emit(AnWave *A, uint64_t pos, uint32_t comb, int wU, int t, int nkern,
+                                        uint64_t ifrom, uint64_t BM, double l0, const uint8_t *ordl,
+                                        const double *ap) {
+    for (uint32_t ks = 0; ks < (1u << nkern); ++ks) {
+        uint32_t DR = comb;
+#pragma unroll
+        for (int q = 0; q < kAnKern; ++q)
+            if (q < nkern && ((ks >> q) & 1u)) DR ^= A->kern[q];
+        const int r = t - wU;
+        uint32_t ifirst;
+        if (__popc(DR) <= r) {
+            ifirst = (wU == 0 && DR == 0u) ? 1u : 0u;  // c = yH: the hard decision fails
+        } else {
+            uint32_t v = DR;
+#pragma unroll
+            for (int k = 0; k < TMAX; ++k)
+                if (k < r) v &= ~(1u << (31 - __builtin_clz(v)));
+            ifirst = v;
+        }
+        if ((uint64_t)ifirst < ifrom || (uint64_t)ifirst >= BM) continue;
+        uint64_t D = pos;
+        for (uint32_t v = DR; v; v &= v - 1) D |= 1ull << ordl[__builtin_ctz(v)];
+        double l = 0.0;  // calcL (:69-77): index order
+        for (uint64_t v = D; v; v &= v - 1) l += ap[__builtin_ctzll(v)];
+        if (!(l < l0)) continue;
+        const uint32_t slot = atomicAdd(&A->ncand, 1u);
+        if (slot < (uint32_t)kAnCand) {
+            AnCand c;
+            c.D = D;
+            c.l = l;
+            c.i = ifirst;
+            c.m = (uint32_t)__popcll(D);
+            A->cand[slot] = c;
+        }
+    }
+}
+
+// Depth-first enumeration of D_U (sum <= limfix, |D_U| <= t) from the root residual. Every
+// lane owns one node whose children it generates, one per step, in ascending order (the
+// first child over the bound ends the node: the reliabilities ascend); children that can
+// have children of their own go on the wave's LDS stack, and lanes without a node take
+// the stack's top entries. So each step visits up to 64 nodes. Returns false when the node
+// budget or the stack runs out (the candidate list is then partial).
+template <int TMAX>
+__device__ bool an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t rem0, uint32_t comb0,
+                             int nkern, uint64_t ifrom, uint64_t BM, double l0, const uint8_t *ordl,
+                             const double *ap, uint32_t budget, int lane, uint32_t &iters) {
+    if (lane == 0) A->ncand = 0u;
+    wave_sync();
+    if (lane == 0 && rem0 == 0ull) an_emit<TMAX>(A, 0ull, comb0, 0, t, nkern, ifrom, BM, l0, ordl, ap);
+    AnNode nd;  // lane 0 starts on the root
+    nd.rem = rem0;
+    nd.pos = 0;
+    nd.sum = 0;
+    nd.sel = 0;
+    nd.comb = comb0;
+    bool have = lane == 0 && t >= 1;
+    int next = 0, sp = 0;
+    uint32_t nodes = 1;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (;;) {
+        const uint64_t idle = ballot(!have);
+        const int nidle = __popcll(idle);
+        const int take = nidle < sp ? nidle : sp;
+        if (!have) {
+            const int k = __popcll(idle & below);
+            if (k < take) {
+                nd = A->stack[sp - 1 - k];
+                have = true;
+                next = 32 - __builtin_clz(nd.sel);  // stacked nodes are non-empty
+            }
+        }
+        sp -= take;
+        if (ballot(have) == 0ull) break;
+        ++iters;
+        wave_sync();  // the pops are read before this step's pushes reuse their slots
+        const int depth = __popc(nd.sel);
+        const int q = next < NU ? next : NU;  // NU: the sentinel (never fits)
+        const bool valid = have && next < NU && depth < t && A->afix[q] <= limfix - nd.sum;
+        have = valid;  // a node ends at its first child over the bound
+        nodes += (uint32_t)__popcll(ballot(valid));
+        const int qc = valid ? q : 0;
+        const int64_t cs = nd.sum + A->afix[qc];
+        const uint64_t crem = nd.rem ^ A->ru[qc];
+        const uint32_t ccomb = nd.comb ^ A->cu[qc];
+        const uint64_t cpos = nd.pos | (1ull << A->pu[qc]);
+        if (valid && crem == 0ull)
+            an_emit<TMAX>(A, cpos, ccomb, depth + 1, t, nkern, ifrom, BM, l0, ordl, ap);
+        const bool expand = valid && depth + 1 < t && qc + 1 < NU && A->afix[qc + 1] <= limfix - cs;
+        const uint64_t em = ballot(expand);
+        const int cnt = __popcll(em);
+        if (sp + cnt > kAnStack) return false;
+        if (expand) {
+            AnNode c;
+            c.rem = crem;
+            c.pos = cpos;
+            c.sum = cs;
+            c.sel = nd.sel | (1u << qc);
+            c.comb = ccomb;
+            A->stack[sp + __popcll(em & below)] = c;
+        }
+        sp += cnt;
+        ++next;
+        wave_sync();
+        if (nodes > budget) return false;
+    }
+    return A->ncand <= (uint32_t)kAnCand;
+}
+
+// First chunk boundary at or after the earliest candidate with l <= lim (~0 if none): from
+// that candidate's pattern on, l0 <= lim.
+__device__ __forceinline__ uint64_t an_earliest(const AnWave *A, double lim, int lane) {
+    const uint32_t nc = A->ncand;
+    uint32_t best = 0xFFFFFFFFu;
+    if ((uint32_t)lane < nc) {
+        const AnCand c = A->cand[lane];
+        if (c.l <= lim) best = c.i;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t x = (uint32_t)__shfl_xor((int)best, o, 64);
+        best = x < best ? x : best;
+    }
+    return best == 0xFFFFFFFFu ? ~0ull : (((uint64_t)best + 63ull) & ~63ull);
+}
+
+struct AnPlan {
+    int mode;       // 0: hand off, 1: candidates complete from ifrom, 2: exact below stop
+    uint64_t stop;  // mode 2: first pattern the replay takes over (a chunk boundary)
+    int why;        // mode 0: 1 geometry, 2 kernel dimension, 3 no split within the
+                    // budget, 4 split too far, 5 re-enumeration failed
+};
+
+// Plan the rest of the search of one codeword from pattern ifrom (a chunk boundary, every
+// earlier pattern processed exactly); candidates land in A.
+template <int M, int TMAX>
+__device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const SearchParams &p,
+                          AnWave *A, const uint32_t *col, const uint8_t *ordl, const double *ap,
+                          uint64_t ifrom, int lane, uint32_t &iters) {
+    constexpr int N = Geo<M>::N, W = Prep<M, TMAX>::W;
+    const int t = p.t, J = p.J;
+    AnPlan plan{0, 0, 0};
+    // NB pattern bits: every pattern any future bound admits, and |U| <= 32
+    int NB;
+    if (N >= 63) NB = 31;
+    else NB = (J >= 0 && J < 31 && S.impr > 0) ? (J < N ? J : N) : (N < 31 ? N : 31);
+    const int NU = N - NB;
+    if (NU > kAnMaxU || NU < 0) { plan.why = 1; return plan; }
+    uint64_t BM;  // patterns at or past BM are never processed
+    if (S.impr == 0) BM = S.bound;
+    else BM = (J >= 0 && J < 31) ? (1ull << J) - 1ull : 0x7FFFFFFFull;
+    if (NB < 31 && BM > (1ull << NB)) { plan.why = 1; return plan; }
+    // Gaussian elimination over GF(2), one column per lane: lanes r < NB the flip columns
+    // (rank r), NB <= r < N the U columns, lane N the hard decision's syndrome S0
+    uint64_t v = 0;
+    if (lane < N) {
+        const int pos = P.ordv[0];
+#pragma unroll
+        for (int w = 0; w < W; ++w) v |= (uint64_t)col[pos * W + w] << (32 * w);
+    } else if (lane == N) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) v |= (uint64_t)P.S0[w] << (32 * w);
+    }
+    uint32_t comb = lane < NB ? (1u << lane) : 0u;
+    bool used = false;
+#pragma unroll
+    for (int q = 0; q < TMAX; ++q) {
+        if (q >= t) break;
+#pragma unroll
+        for (int b = 0; b < M; ++b) {
+            const int bit = 8 * q + b;
+            const bool has = (v >> bit) & 1ull;
+            const uint64_t cm = ballot(has && lane < NB && !used);
+            if (!cm) continue;
+            const int k = (int)__builtin_ctzll(cm);
+            const uint64_t pv = rdl64(v, k);
+            const uint32_t pc = rdl(comb, k);
+            if (has && lane != k) {
+                v ^= pv;
+                comb ^= pc;
+            }
+            used = used || lane == k;
+        }
+    }
+    const uint64_t km = ballot(lane < NB && !used);  // dependent flip columns: the kernel
+    const int nkern = __popcll(km);
+    if (nkern > kAnKern) { plan.why = 2; return plan; }
+    {
+        uint64_t kk = km;
+        for (int q = 0; q < nkern; ++q) {
+            const int k = (int)__builtin_ctzll(kk);
+            kk &= kk - 1;
+            const uint32_t kc = rdl(comb, k);
+            if (lane == 0) A->kern[q] = kc;
+        }
+    }
+    const uint64_t rem0 = rdl64(v, N);
+    const uint32_t comb0 = rdl(comb, N);
+    if (lane >= NB && lane < N) {
+        const int q = lane - NB;
+        A->afix[q] = an_fix(P.asv[0]);
+        A->ru[q] = v;
+        A->cu[q] = comb;
+        A->pu[q] = (uint8_t)P.ordv[0];
+    }
+    if (lane == 0) A->afix[NU] = (int64_t)0x7FFFFFFFFFFFFFFFll;
+    wave_sync();
+    const double l0 = S.l0;
+    const double full = l0 * (1.0 + 0x1p-40);
+    if (an_enumerate<TMAX>(A, NU, t, an_fix_up(full), rem0, comb0, nkern, ifrom, BM, l0, ordl, ap, kAnBudget,
+                           lane, iters)) {
+        plan.mode = 1;
+        return plan;
+    }
+    // tighter bounds lim_k = the sum of the k least reliable U positions, ascending k (the
+    // enumeration grows ~5x per step): the largest k within the budget whose earliest
+    // candidate with l <= lim_k comes first wins; the exact chunks then end at its pattern
+    const int kmax = (t + 1 < NU ? t + 1 : NU);
+    int best_k = 0, cur_k = 0;
+    uint64_t best_stop = 0;
+    double lim = 0.0;
+    for (int k = 1; k <= kmax; ++k) {
+        lim += rdlf(P.asv[0], NB + k - 1);
+        if (!(lim < full)) break;  // no tighter than l0 (that attempt failed)
+        cur_k = k;
+        if (!an_enumerate<TMAX>(A, NU, t, an_fix_up(lim * (1.0 + 0x1p-40)), rem0, comb0, nkern, ifrom, BM, l0,
+                                ordl, ap, kAnBudget, lane, iters))
+            break;
+        const uint64_t stop = an_earliest(A, lim, lane);
+        if (stop == ~0ull) continue;
+        best_k = k;
+        best_stop = stop;
+        if (stop <= ifrom + 64ull) break;  // cannot end sooner
+    }
+    if (best_k == 0 || best_stop - ifrom > 64ull * kAnExactChunks) {
+        plan.why = best_k == 0 ? 3 : 4;
+        return plan;
+    }
+    if (cur_k != best_k) {  // the list holds a later attempt: enumerate best_k again
+        double lb = 0.0;
+        for (int q = 0; q < best_k; ++q) lb += rdlf(P.asv[0], NB + q);
+        if (!an_enumerate<TMAX>(A, NU, t, an_fix_up(lb * (1.0 + 0x1p-40)), rem0, comb0, nkern, ifrom, BM, l0,
+                                ordl, ap, kAnBudget, lane, iters))
+            { plan.why = 5; return plan; }
+    }
+    plan.mode = 2;
+    plan.stop = best_stop;
+    return plan;
+}
+
+// The reference loop from pattern `from` on, over the candidates (first patterns >= from)
+// in pattern order; the loop ends at its bound or, chunk-granular, at the decode cap.
+template <int M, int TMAX>
+__device__ void an_replay(SearchState<1> &S, const Prep<M, TMAX> &P, const AnWave *A, uint64_t from,
+                          const double *as, const SearchParams &p, int lane) {
+    const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63ull) & ~63ull) : ~0ull;
+    const uint32_t nc = A->ncand < (uint32_t)kAnCand ? A->ncand : (uint32_t)kAnCand;
+    uint64_t key[1] = {~0ull};
+    if ((uint32_t)lane < nc && (uint64_t)A->cand[lane].i >= from)
+        key[0] = ((uint64_t)A->cand[lane].i << 6) | (uint64_t)lane;
+    wave_bitonic_sort<1>(key, lane);
+    for (int k = 0; k < 64; ++k) {
+        const uint64_t kk = rdl64(key[0], k);
+        if (kk == ~0ull) break;
+        const uint64_t ii = kk >> 6;
+        if (ii >= S.bound || ii >= capc) break;
+        const AnCand c = A->cand[kk & 63ull];
+        Mask<1> d;
+        d.w[0] = c.D;
+        accept_success<M, TMAX>(S, P, d, (int)c.m, c.l, ii, as, p, lane);
+        if (S.done) return;
+    }
+    if (((S.bound + 63ull) & ~63ull) <= capc) {
+        S.i_end = S.bound;
+    } else {
+        S.i_end = capc;
+        S.truncated = true;
+    }
+    S.done = true;
+}
+
 // ------------------------------------------------ wave-per-codeword search
 // 64 consecutive test patterns per step, acceptance in pattern order. A codeword still
-// running after p.chunk_limit steps is handed to the cooperative kernel (heavy queue).
-template <int M, int TMAX, bool TAB>
+// running after p.chunk_limit steps finishes through the analytic tail (above) or is handed
+// to the cooperative kernel (heavy queue).
+template <int M, int TMAX, bool TAB, bool AN>
 __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const uint16_t *lg,
                                 const uint32_t *col, const uint64_t *chien, double *as,
-                                double *ap, uint8_t *ordl, uint32_t cw, int lane) {
+                                double *ap, uint8_t *ordl, uint32_t cw, int lane, AnWave *an) {
     constexpr int NW = Geo<M>::NW;
+    // analytic tail: exact chunks end at an_stop, then the candidates decide the rest
+    bool an_tried = false, an_exact = false;
+    uint64_t an_stop = 0;
+    (void)an_tried;
+    // analytic-tail timing records (p.tail_diag, diagnostics only): cycles per phase
+    uint64_t dg_t0 = 0, dg_t1 = 0, dg_t2 = 0, dg_t3 = 0;
+    uint32_t dg_iters = 0, dg_mode = 0;
+    if (AN && p.tail_diag) dg_t0 = __builtin_amdgcn_s_memtime();
     Prep<M, TMAX> P;
     prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+    if (AN && p.tail_diag) dg_t1 = __builtin_amdgcn_s_memtime();
     SearchState<NW> S;
     init_state<M>(S, p.variant);
+    (void)an;
+    auto tail_record = [&]() {
+        if (AN && p.tail_diag && an_tried && lane == 0) {
+            const uint32_t r = atomicAdd(p.tail_diag_count, 1u);
+            if (r < p.tail_diag_cap) {
+                unsigned long long *d = p.tail_diag + (size_t)r * 8;
+                const uint64_t t4 = __builtin_amdgcn_s_memtime();
+                d[0] = cw;
+                d[1] = dg_t1 - dg_t0;
+                d[2] = dg_t2 - dg_t1;
+                d[3] = dg_t3 - dg_t2;
+                d[4] = dg_iters;
+                d[5] = dg_mode;
+                d[6] = t4 - dg_t3;
+                d[7] = S.i_end;
+            }
+        }
+    };
     if constexpr (M >= 7) {
         // long codes: the first test patterns one at a time, unless kaneko_first_kernel has
         // done so already (it queued this codeword)
@@ -584,12 +959,46 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         // the checks of the next chunk before any decode (no group started past the end)
         if (base0 >= S.bound) { S.i_end = S.bound; break; }
         if (p.max_decodes && base0 >= p.max_decodes) { S.i_end = base0; S.truncated = true; break; }
+        if constexpr (AN && an_capable<M, TMAX>() && G == 1) {
+            if (p.analytic && p.heavy_tail && chunks >= p.chunk_limit && !an_tried &&
+                p.variant == BCHK_VARIANT_ANSWER) {
+                an_tried = true;
+                uint32_t iters = 0;
+                if (p.tail_diag) dg_t2 = __builtin_amdgcn_s_memtime();
+                const AnPlan plan = an_plan<M, TMAX>(S, P, p, an, col, ordl, ap, base0, lane, iters);
+                if (p.tail_diag) {
+                    dg_t3 = __builtin_amdgcn_s_memtime();
+                    dg_iters = iters;
+                    dg_mode = (uint32_t)plan.mode | ((uint32_t)plan.why << 8) |
+                              (uint32_t)(((plan.stop > base0 ? plan.stop - base0 : 0) >> 6) << 16);
+                }
+                if (p.tail_stats && lane == 0) {
+                    atomicAdd(p.tail_stats + plan.mode, 1u);
+                    if (plan.mode == 2) atomicAdd(p.tail_stats + 3, (uint32_t)((plan.stop - base0) >> 6));
+                    atomicAdd(p.tail_stats + 4, iters);
+                    atomicMax(p.tail_stats + 5, iters);
+                }
+                if (plan.mode == 1) {
+                    an_replay<M, TMAX>(S, P, an, base0, as, p, lane);
+                    break;
+                }
+                if (plan.mode == 2) {
+                    an_exact = true;
+                    an_stop = plan.stop;
+                }
+            }
+            if (an_exact && base0 >= an_stop) {
+                an_replay<M, TMAX>(S, P, an, an_stop, as, p, lane);
+                break;
+            }
+        }
+        const bool hand_off = p.heavy_tail && chunks >= p.chunk_limit && !an_exact;
         Mask<NW> diff[G];
         int m[G];
         double l[G];
         bool ok[G];
         bool handed = false;
-        if (!(p.heavy_tail && chunks >= p.chunk_limit))
+        if (!hand_off)
             decode_chunks<M, TMAX, G, TAB>(P, base0, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok);
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -601,7 +1010,7 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
                 S.done = true;
                 break;
             }
-            if (p.heavy_tail && chunks >= p.chunk_limit) {
+            if (hand_off) {
                 if (lane == 0) {  // longest-first: large remaining bounds to the front queue
                     uint32_t *slot = S.bound >= p.heavy_big
                                          ? p.heavy_queue + atomicAdd(p.heavy_tail, 1u)
@@ -636,10 +1045,14 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
             }
             if (S.done) break;
         }
-        if (handed) return;
+        if (handed) {
+            tail_record();
+            return;
+        }
         if (S.done) break;
     }
     write_outputs<M, TMAX>(S, P, p, cw, lane);
+    tail_record();
 }
 
 // Relaxed device-scope atomics only: acquire/release at agent scope would write back or
@@ -664,7 +1077,7 @@ __device__ __forceinline__ void wave_done(const SearchParams &p, int lane, uint3
     }
 }
 
-template <int M, int TMAX, bool TAB>
+template <int M, int TMAX, bool TAB, bool AN>
 __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock)
 kaneko_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -676,15 +1089,18 @@ kaneko_search_kernel(SearchParams p) {
     const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int NP = Smem<M, TMAX>::NP;
-    uint8_t *wbase = smem + ((p.td.bytes + 15) & ~15u) + wid * Smem<M, TMAX>::WAVE_BYTES;
+    // per wave: the prep's LDS slice, then the analytic tail's state (n <= 63)
+    constexpr int WB = Smem<M, TMAX>::WAVE_BYTES, SB = WB + (AN ? an_bytes<M, TMAX>() : 0);
+    uint8_t *wbase = smem + ((p.td.bytes + 15) & ~15u) + wid * SB;
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
+    AnWave *an = (AN && an_capable<M, TMAX>()) ? reinterpret_cast<AnWave *>(wbase + WB) : nullptr;
     if (!p.queue) {
         const uint32_t stride = gridDim.x * kWavesPerBlock;
         uint32_t ndone = 0;
         for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride, ++ndone)
-            search_codeword<M, TMAX, TAB>(p, ex, lg, col, chien, as, ap, ordl, cw, lane);
+            search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an);
         wave_done(p, lane, ndone);
         return;
     }
@@ -704,7 +1120,7 @@ kaneko_search_kernel(SearchParams p) {
             ++exhausted;
             continue;
         }
-        search_codeword<M, TMAX, TAB>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane);
+        search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane, an);
         ++ndone;
     }
     wave_done(p, lane, ndone);
@@ -1193,9 +1609,9 @@ __global__ void __launch_bounds__(256) count_kernel(const uint8_t *tx, const uin
 }
 
 // ------------------------------------------------------------- launchers
-template <int M, int TMAX, bool TAB>
+template <int M, int TMAX, bool TAB, bool AN>
 static hipError_t launch_search_impl(const SearchParams &p, int grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((kaneko_search_kernel<M, TMAX, TAB>), dim3(grid),
+    hipLaunchKernelGGL((kaneko_search_kernel<M, TMAX, TAB, AN>), dim3(grid),
                        dim3(kWaveSize * kWavesPerBlock), lds, s, p);
     return hipGetLastError();
 }
@@ -1211,8 +1627,8 @@ static hipError_t launch_alg_impl(const AlgParams &p, size_t lds, hipStream_t s)
     hipLaunchKernelGGL((alg_decode_kernel<M, TMAX>), dim3(grid), dim3(256), lds, s, p);
     return hipGetLastError();
 }
-template <int M, int TMAX, bool TAB>
-static const void *search_fn() { return reinterpret_cast<const void *>(&kaneko_search_kernel<M, TMAX, TAB>); }
+template <int M, int TMAX, bool TAB, bool AN>
+static const void *search_fn() { return reinterpret_cast<const void *>(&kaneko_search_kernel<M, TMAX, TAB, AN>); }
 template <int M, int TMAX, bool TAB>
 static const void *coop_fn() { return reinterpret_cast<const void *>(&kaneko_coop_kernel<M, TMAX, TAB>); }
 
@@ -1243,15 +1659,24 @@ static KernelSet make_set() {
     const size_t coop = sizeof(CoopSlot<NW>) * coop_slots<NW>() + sizeof(CoopCtl) +
                         (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES;
     KernelSet k{};
-    k.search = &launch_search_impl<M, TMAX, false>;
+    k.search = &launch_search_impl<M, TMAX, false, false>;
     k.coop = &launch_coop_impl<M, TMAX, false>;
     k.coop_ptr = &coop_fn<M, TMAX, false>;
-    k.search_ptr = &search_fn<M, TMAX, false>;
+    k.search_ptr = &search_fn<M, TMAX, false, false>;
     if constexpr (tab_capable<M, TMAX>()) {
-        k.search_tab = &launch_search_impl<M, TMAX, true>;
+        k.search_tab = &launch_search_impl<M, TMAX, true, false>;
         k.coop_tab = &launch_coop_impl<M, TMAX, true>;
         k.coop_tab_ptr = &coop_fn<M, TMAX, true>;
-        k.search_tab_ptr = &search_fn<M, TMAX, true>;
+        k.search_tab_ptr = &search_fn<M, TMAX, true, false>;
+    }
+    if constexpr (an_capable<M, TMAX>()) {
+        k.tail = &launch_search_impl<M, TMAX, false, true>;
+        k.tail_ptr = &search_fn<M, TMAX, false, true>;
+        if constexpr (tab_capable<M, TMAX>()) {
+            k.tail_tab = &launch_search_impl<M, TMAX, true, true>;
+            k.tail_tab_ptr = &search_fn<M, TMAX, true, true>;
+        }
+        k.tail_wave_bytes = (size_t)(Smem<M, TMAX>::WAVE_BYTES + an_bytes<M, TMAX>());
     }
     k.coop_bytes = coop;
     k.alg = &launch_alg_impl<M, TMAX>;
@@ -1277,6 +1702,9 @@ bool select_kernels(int m, int t, KernelSet *out) {
 
 hipError_t launch_search(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s) {
     return (p.tab.slots && k.search_tab) ? k.search_tab(p, grid, lds, s) : k.search(p, grid, lds, s);
+}
+hipError_t launch_tail(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s) {
+    return (p.tab.slots && k.tail_tab) ? k.tail_tab(p, grid, lds, s) : k.tail(p, grid, lds, s);
 }
 hipError_t launch_coop(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s) {
     return (p.tab.slots && k.coop_tab) ? k.coop_tab(p, grid, lds, s) : k.coop(p, grid, lds, s);

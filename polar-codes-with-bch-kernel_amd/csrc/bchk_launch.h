@@ -21,6 +21,14 @@ struct KernelSet {
     hipError_t (*alg)(const AlgParams &, size_t, hipStream_t);
     int tmax;
     size_t wave_bytes;  // LDS bytes per wave of the search kernel
+    // analytic-tail instance of the search kernel (n <= 63, TMAX <= 8; null elsewhere): it
+    // takes the codewords the first pass hands off and finishes them from their candidate
+    // codewords, handing only the rest on to the cooperative kernel
+    hipError_t (*tail)(const SearchParams &, int, size_t, hipStream_t);
+    hipError_t (*tail_tab)(const SearchParams &, int, size_t, hipStream_t);
+    const void *(*tail_ptr)();
+    const void *(*tail_tab_ptr)();
+    size_t tail_wave_bytes;
 };
 
 typedef hipError_t (*FastFn)(const SearchParams &, size_t, hipStream_t);
@@ -37,6 +45,7 @@ bool select_kernels(int m, int t, KernelSet *out);
 // search / cooperative kernel: the table variant when p.tab.slots is set and it exists
 hipError_t launch_search(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s);
 hipError_t launch_coop(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s);
+hipError_t launch_tail(const KernelSet &k, const SearchParams &p, int grid, size_t lds, hipStream_t s);
 constexpr int kCoopThreads = 1024;
 hipError_t launch_alg(const KernelSet &k, const AlgParams &p, size_t lds, hipStream_t s);
 hipError_t launch_count(int n, const uint8_t *tx, const uint8_t *res, const bchk_stats *st,

@@ -16,23 +16,26 @@ _ctx = {}
 
 
 # execution paths, all of which must give the reference's results:
-#   "fast+exact+coop"  default: lane-per-codeword fast path, wave-per-codeword exact kernel,
-#                      workgroup-cooperative kernel after 4 chunks
-#   "exact-only"       no fast path, no cooperative hand-off (one wave per codeword)
-#   "coop-heavy"       cooperative hand-off after the first chunk
+#   "fast+exact+tail"  default: lane-per-codeword fast path, wave-per-codeword exact kernel,
+#                      after 2 chunks the analytic tail kernel (candidate codewords,
+#                      csrc/bchk_kernels.hip), the cooperative kernel for what it hands on
+#   "exact-only"       no fast path, no hand-off (one wave per codeword, every pattern)
+#   "tail-early"       analytic tail after the first chunk
+#   "coop-heavy"       no analytic tail: cooperative hand-off after the first chunk
 #   "no-table"         default paths with Berlekamp-Massey + Chien for every test pattern
 #                      instead of the syndrome decoding table (csrc/bchk_syndtab.h)
-PATHS = {"fast+exact+coop": (True, None, True), "exact-only": (False, "0", True),
-         "coop-heavy": (True, "1", True), "no-table": (True, None, False)}
+PATHS = {"fast+exact+tail": (True, None, True, True), "exact-only": (False, "0", True, True),
+         "tail-early": (True, "1", True, True), "coop-heavy": (True, "1", True, False),
+         "no-table": (True, None, False, True)}
 
 
 def dec(m, t, J=-1, fast=True, path=None):
-    filt = True
+    filt, analytic = True, True
     if path is not None:
-        fast, limit, filt = PATHS[path]
+        fast, limit, filt, analytic = PATHS[path]
     else:
         limit = None
-    key = (m, t, J, fast, limit, filt)
+    key = (m, t, J, fast, limit, filt, analytic)
     if key not in _ctx:
         old = os.environ.pop("BCHK_CHUNK_LIMIT", None)
         if limit is not None:
@@ -45,6 +48,7 @@ def dec(m, t, J=-1, fast=True, path=None):
                 os.environ["BCHK_CHUNK_LIMIT"] = old
         d.set_fast_path(fast)
         d.set_syndrome_table(filt)
+        d.set_analytic(analytic)
         _ctx[key] = d
     return _ctx[key]
 
@@ -251,8 +255,15 @@ def test_path_counts_and_profile_report_each_stage():
     ms, calls = d.profile_read()
     d.profile(False)
     to_exact, to_coop = d.path_counts()
+    to_tail = d.tail_count()
     assert calls == 1 and len(ms) == 3 and ms[0] > 0 and ms[1] > 0
-    assert 0 < to_exact < (1 << 14) and 0 < to_coop <= to_exact
+    assert 0 < to_exact < (1 << 14) and 0 < to_tail <= to_exact and to_coop <= to_tail
+    # per stage, with the analytic tail kernel as its own stage
+    d.profile(True)
+    d.decode(y)
+    ms4, calls = d.profile_read_stages()
+    d.profile(False)
+    assert calls == 1 and len(ms4) == 4 and ms4[3] > 0
 
 
 @pytest.mark.parametrize("m,t", [(4, 2), (5, 3), (6, 6), (6, 4), (5, 7)])
