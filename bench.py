@@ -4,16 +4,17 @@
 A step = one pass of the hot path over one resident batch: Kaneko decode of B codewords
 (libbchk search kernel) + FER/op counter reduction (+ one RCCL all-reduce of the 6
 counters when N > 1). Inputs are the reference's own channel stream (minstd_rand0 +
-libstdc++ distributions, rank-specific seed), generated on the host and resident in HBM
+libstdc++ distributions; rank r starts (2^31-2)/N draws after rank r-1 in it), generated on the host and resident in HBM
 before timing. Weak scaling: every rank decodes its own B codewords.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints one JSON line (driver contract) with `roofline` (HIP-event kernel time of
-the search kernel vs the 8 TB/s HBM roof at 9n+8 algorithmic bytes per codeword) and
-`cpu_baseline` (the reference itself, compiled into oracle/_ref, timed on one host core on
-a bounded sample of the same workload).
+the dominant kernel vs the 8 TB/s HBM roof at 9n+8 algorithmic bytes per codeword),
+`points` (the same measurement at each Eb/N0 of --points: the FER/throughput curve) and
+`cpu_baseline` (the reference itself, compiled into oracle/_ref, one process per host core
+on disjoint ranges of the same stream, on a bounded sample of the same workload).
 """
 import argparse
 import json
@@ -36,12 +37,16 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--m", type=int, default=6)
     ap.add_argument("--t", type=int, default=6)
-    ap.add_argument("--snr", type=float, default=5.0, help="Eb/N0 in dB")
+    ap.add_argument("--snr", type=float, default=5.0, help="Eb/N0 in dB (the headline point)")
+    ap.add_argument("--points", default="4,5,6",
+                    help="Eb/N0 points (dB) of the FER/throughput curve; '' = the headline only")
     ap.add_argument("--J", type=int, default=15, help="test-pattern cap; -1 = shipped (uncapped)")
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="target CPU time of the cpu_baseline sample (0 = skip)")
+                    help="target wall time of the cpu_baseline sample (0 = skip)")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="reference processes for the CPU baseline (0 = the host's core share)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -62,9 +67,19 @@ def dec_tmax(t):
     return t if t in (1, 2, 3, 6, 15) else next(b for b in (7, 8, 12, 16, 31, 32) if b >= t)
 
 
-def rank_seed(seed, rank):
-    """Disjoint per-rank input streams: rank r decodes the stream seeded seed + 7919 r."""
-    return seed + 7919 * rank
+def rank_stream_start(bchk, seed, rank, world):
+    """Rank r decodes draws [r D, r D + used) of the one reference stream (minstd_rand0 from
+    `seed`), D = the engine period / world: a jump-ahead, so the ranks' inputs never overlap
+    as long as every rank uses at most D draws (checked by check_rank_draws)."""
+    D = bchk.MINSTD_PERIOD // world
+    return bchk.rng_jump(seed, rank * D), D
+
+
+def check_rank_draws(used, budget, world):
+    if used > budget:
+        raise SystemExit(f"rank stream overlap: one batch uses {used} engine draws, more than the "
+                         f"{budget} per rank that {world} ranks leave in minstd_rand0's period 2^31-2; "
+                         "use fewer codewords per rank")
 
 
 def reduce_step(step_cnt, total_cnt, world, dist):
@@ -83,8 +98,18 @@ def max_over_ranks(value, world, dist, device):
     return float(t.item())
 
 
-def cpu_baseline(args, gpu_rate):
-    """The reference decode(answer, word, res) on one host core, same code/SNR/J."""
+def host_cores():
+    """CPUs this process may use: its affinity set, capped by the job share the GPU box
+    exports (OMP_NUM_THREADS = 16 there: os.cpu_count() is the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(share))) if share and share.isdigit() else max(1, n)
+
+
+def cpu_baseline(args, gpu_rate, bchk):
+    """The reference decode(answer, word, res) timed on the host's cores: one reference
+    process per core, each on its own range of the reference stream (jump-ahead), same
+    code/SNR/J; per-core and aggregate codewords/s."""
     if args.cpu_seconds <= 0:
         return None
     exe = os.path.join(REPO, "oracle", "_ref", "ref_golden_j15" if args.J == 15 else "ref_golden")
@@ -94,14 +119,34 @@ def cpu_baseline(args, gpu_rate):
     # size the sample from a short probe so the whole leg takes ~cpu_seconds
     probe = 2000
     if exe:
-        def run(count):
-            out = subprocess.run([exe, "bench", str(args.m), str(args.t), str(args.seed), str(count),
-                                  repr(args.snr)], capture_output=True, text=True, check=True).stdout
-            return json.loads(out.strip().splitlines()[-1])
-        r = run(probe)
+        procs = args.cpu_procs or host_cores()
+
+        def cmd(seed, count):
+            return [exe, "bench", str(args.m), str(args.t), str(seed), str(count), repr(args.snr)]
+
+        r = json.loads(subprocess.run(cmd(args.seed, probe), capture_output=True, text=True,
+                                      check=True).stdout.strip().splitlines()[-1])
         count = int(max(probe, min(2_000_000, r["codewords_per_s"] * args.cpu_seconds)))
-        r = run(count)
-        rate, words = r["codewords_per_s"], r["words"]
+        span = bchk.MINSTD_PERIOD // procs  # disjoint stream ranges (>> count words' draws)
+        ps = [subprocess.Popen(cmd(bchk.rng_jump(args.seed, i * span), count), stdout=subprocess.PIPE,
+                               text=True) for i in range(procs)]
+        t0 = time.perf_counter()
+        outs = [json.loads(pp.communicate()[0].strip().splitlines()[-1]) for pp in ps]
+        wall = time.perf_counter() - t0
+        if any(pp.returncode for pp in ps):
+            raise RuntimeError("reference baseline process failed")
+        per_core = [o["codewords_per_s"] for o in outs]
+        # aggregate: all words over the slowest process's decode time (generation excluded)
+        rate = procs * count / max(o["seconds"] for o in outs)
+        return {"value": round(rate, 3), "unit": "codewords/s", "cores": procs,
+                "nproc": os.cpu_count(), "per_core": round(sum(per_core) / procs, 3),
+                "per_core_min": round(min(per_core), 3), "kind": kind,
+                "sample": f"{procs} reference processes x {count} codewords, each from its own "
+                          f"range of the reference stream (seed {args.seed}, jump-ahead), "
+                          f"Eb/N0={args.snr} dB, J={'inf' if args.J < 0 else args.J}, "
+                          f"BCH({(1 << args.m) - 1}) t={args.t}; decode calls only; wall "
+                          f"{wall:.1f} s incl. generation",
+                "gpu_over_cpu": round(gpu_rate / rate, 1) if rate > 0 else None}
     else:
         from oracle_lib import Oracle
         o = Oracle(args.m, args.t)
@@ -114,34 +159,29 @@ def cpu_baseline(args, gpu_rate):
         t0 = time.perf_counter()
         o.kaneko_batch(y, J=args.J)
         rate, words = count / (time.perf_counter() - t0), count
-    return {"value": round(rate, 3), "unit": "codewords/s", "cores": 1, "kind": kind,
+    return {"value": round(rate, 3), "unit": "codewords/s", "cores": 1, "nproc": os.cpu_count(),
+            "kind": kind,
             "sample": f"first {words} codewords of the reference stream (seed {args.seed}) at "
                       f"Eb/N0={args.snr} dB, J={'inf' if args.J < 0 else args.J}, BCH("
                       f"{(1 << args.m) - 1}) t={args.t}; decode calls only, 1 thread",
             "gpu_over_cpu": round(gpu_rate / rate, 1) if rate > 0 else None}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def run_point(args, bchk, dec, snr, world, rank, dist, dev):
+    """One Eb/N0 point: the rank's batch generated into HBM, W warmup + K timed steps (max over
+    ranks), per-kernel HIP-event durations from K more steps, FER/op counters."""
     import numpy as np
     import torch
-    import torch.distributed as dist
 
-    bchk = load_pkg()
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dec = bchk.KanekoKernelProcessor(args.m, args.t, J=args.J, device=local)
     n, B = dec.n, args.batch
+    start, budget = rank_stream_start(bchk, args.seed, rank, world)
     t_gen = time.perf_counter()
-    tx, y, _ = dec.generate(args.snr, B, seed=rank_seed(args.seed, rank))
+    tx, y, _, used = dec.generate_draws(snr, B, state=start)
     t_gen = time.perf_counter() - t_gen
-    dev = torch.device("cuda", local)
+    check_rank_draws(used, budget, world)
     d_y = torch.from_numpy(y).to(dev)
     d_tx = torch.from_numpy(tx).to(dev)
+    del tx, y
     d_res = torch.zeros((B, n), dtype=torch.uint8, device=dev)
     d_l0 = torch.empty(B, dtype=torch.float64, device=dev)
     d_st = torch.empty((B, bchk.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
@@ -183,85 +223,134 @@ def main():
             step()
         dec.sync()
         torch.cuda.synchronize()
-    ms3, launches = dec.profile_read()  # launches: sub-batch launches per stage
+    ms4, launches = dec.profile_read_stages()  # fast, exact first pass, coop, analytic tail
     dec.profile(False)
     n_exact, n_coop = dec.path_counts()
+    n_tail = dec.tail_count()
+    tail_stats = dec.tail_stats()
     elapsed = max_over_ranks(elapsed, world, dist, dev)
     cnt = d_cnt.cpu().numpy().astype(np.int64)  # summed over ranks (N > 1)
     total_words = world * B * args.steps
     value = total_words / elapsed
     # Algorithmic bytes per codeword: 8n B of f64 samples in, n B decoded bits and 8 B l0
-    # out. The fast kernel moves them for all B codewords; the exact and
-    # cooperative kernels re-read/write them for the codewords handed to them.
+    # out. The fast kernel moves them for all B codewords; the exact, tail
+    # and cooperative kernels re-read/write them for the codewords handed to them.
     bytes_per_cw = 9 * n + 8
     launches = max(1, launches)
-    pipe = max(1, launches // args.steps)  # sub-batches per decode call (stream pipeline)
     tm = dec_tmax(args.t)
     # the lane-per-codeword fast kernel exists for n <= 63 and small t (csrc/bchk_fast.hip
     # select_fast); without it stage 0 is only the control-block memset
     # (n > 63: kaneko_first_kernel, the first test patterns of every codeword)
     has_fast = args.m >= 7 or args.t <= {3: 3, 4: 7, 5: 8, 6: 6}.get(args.m, -1)
     fast_name = "kaneko_fast_kernel" if args.m <= 6 else "kaneko_first_kernel"
-    fast_on = has_fast and ms3[0] > 0 and n_exact < B
+    fast_on = has_fast and ms4[0] > 0 and n_exact < B
     # per launch: average duration (HIP events on the launching stream) and the codewords
-    # one launch processes (the last call's hand-off counts, spread over its sub-batches)
+    # one launch processes
     kern = [{"name": f"{fast_name}<{args.m},{tm}>" if has_fast else "control memset",
-             "ms": ms3[0] / launches, "codewords": B / pipe if has_fast else 0},
-            {"name": f"kaneko_search_kernel<{args.m},{tm}>", "ms": ms3[1] / launches,
-             "codewords": (n_exact if fast_on else B) / pipe},
-            {"name": f"kaneko_coop_kernel<{args.m},{tm}>", "ms": ms3[2] / launches,
-             "codewords": n_coop / pipe}]
+             "ms": ms4[0] / launches, "codewords": B if has_fast else 0},
+            {"name": f"kaneko_search_kernel<{args.m},{tm}>", "ms": ms4[1] / launches,
+             "codewords": n_exact if fast_on else B},
+            {"name": f"kaneko_search_kernel<{args.m},{tm}> analytic tail", "ms": ms4[3] / launches,
+             "codewords": n_tail},
+            {"name": f"kaneko_coop_kernel<{args.m},{tm}>", "ms": ms4[2] / launches,
+             "codewords": n_coop}]
     for k in kern:
         k["GB_s"] = (bytes_per_cw * k["codewords"] / (k["ms"] / 1e3) / 1e9) if k["ms"] > 0 else 0.0
     dom = max(kern, key=lambda k: k["ms"])
-    achieved = dom["GB_s"]
+    words = int(cnt[5])
+    return {
+        "snr_db": snr, "value": value, "ms_per_step": elapsed / args.steps * 1e3,
+        "fer": (int(cnt[0]) / words) if words else None,
+        "ber": (int(cnt[1]) / words / n) if words else None,
+        "frame_errors": int(cnt[0]), "words": words,
+        "decodes_per_codeword": (int(cnt[2]) / words) if words else None,
+        "kernels": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in kk.items()} for kk in kern],
+        "dominant_kernel": dom["name"], "dominant_GB_s": dom["GB_s"],
+        "frac": dom["GB_s"] / HBM_PEAK_GBS,
+        "kernel_ms_per_step": sum(k["ms"] for k in kern),
+        "tail": {"to_tail": n_tail, "finished": tail_stats[1], "split": tail_stats[2],
+                 "handed_on": tail_stats[0], "split_chunks": tail_stats[3],
+                 "enum_steps_max": tail_stats[5]},
+        "host_generation_s": t_gen, "rank_draws": used, "rank_draw_budget": budget,
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    bchk = load_pkg()
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dec = bchk.KanekoKernelProcessor(args.m, args.t, J=args.J, device=local)
+    n, B = dec.n, args.batch
+    dev = torch.device("cuda", local)
+    snrs = [float(x) for x in args.points.split(",") if x.strip()] if args.points else []
+    if args.snr not in snrs:
+        snrs.append(args.snr)
+    pts = {snr: run_point(args, bchk, dec, snr, world, rank, dist, dev) for snr in sorted(snrs)}
+    head = pts[args.snr]
+    dom = next(k for k in head["kernels"] if k["name"] == head["dominant_kernel"])
     # HBM bytes per launch of the dominant kernel, from the committed PMC passes of the same
-    # workload (scripts/gpu_final.sh -> scripts/traffic_json.py): FETCH_SIZE x 2 (gfx950)
-    # + WRITE_SIZE, null when no profile of this workload exists
-    traffic = None
+    # workload (scripts/gpu_final.sh -> scripts/traffic_json.py, rocprofv3 --pmc FETCH_SIZE
+    # x 2 (gfx950) + WRITE_SIZE); null when no profile of this workload exists. It is a
+    # stored measurement (rocprofv3 cannot run inside this process): its source is named.
+    traffic, traffic_src = None, None
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
             if tr.get("batch") == B and tr.get("snr_db") == args.snr and tr.get("J") == args.J:
                 traffic = tr.get("kernels", {}).get(dom["name"].replace(" ", ""))
+                traffic_src = f"{tr.get('source')} ({tr.get('date', 'undated')})"
         except Exception:
             traffic = None
     if rank == 0:
-        words = int(cnt[5])
         out = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": round(head["value"], 3),
             "unit": "codewords/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(head["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: the reference's AWGN stream (minstd_rand0 + libstdc++ "
-                    "distributions), BPSK, generated on host, resident in HBM",
+                    "distributions), BPSK, generated on host, resident in HBM; rank r decodes "
+                    "its own jump-ahead range of the one stream",
             "config": {"workload": f"Kaneko ML soft decoding of BCH({n},{dec.k},{2 * args.t + 1}), "
                                    f"Eb/N0={args.snr} dB, J={'inf' if args.J < 0 else args.J}",
                        "code": f"BCH({n},{dec.k},{2 * args.t + 1})", "batch_per_gpu": B,
                        "global_batch": world * B, "snr_db": args.snr, "J": args.J,
-                       "L": 8, "parallelism": f"dp{world}"},
-            "fer": (int(cnt[0]) / words) if words else None,
-            "ber": (int(cnt[1]) / words / n) if words else None,
-            "decodes_per_codeword": (int(cnt[2]) / words) if words else None,
-            "kernels": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in kk.items()}
-                        for kk in kern],
-            "dominant_kernel": dom["name"],
-            "sub_batches_per_step": pipe,
-            "kernel_ms_per_step": round(pipe * sum(k["ms"] for k in kern), 4),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": traffic},
-            "host_generation_s": round(t_gen, 2),
+                       "L_inert": 8, "parallelism": f"dp{world}"},
+            "fer": head["fer"],
+            "ber": head["ber"],
+            "decodes_per_codeword": head["decodes_per_codeword"],
+            "kernels": head["kernels"],
+            "dominant_kernel": head["dominant_kernel"],
+            "kernel_ms_per_step": round(head["kernel_ms_per_step"], 4),
+            "roofline": {"bound": "hbm", "achieved": round(head["dominant_GB_s"], 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(head["frac"], 6), "traffic": traffic,
+                         "traffic_source": traffic_src},
+            "points": [{"snr_db": p["snr_db"], "value": round(p["value"], 3),
+                        "ms_per_step": round(p["ms_per_step"], 4), "fer": p["fer"],
+                        "frame_errors": p["frame_errors"], "words": p["words"],
+                        "decodes_per_codeword": p["decodes_per_codeword"],
+                        "dominant_kernel": p["dominant_kernel"], "frac": round(p["frac"], 6),
+                        "kernels": p["kernels"], "tail": p["tail"]} for p in pts.values()],
+            "tail": head["tail"],
+            "host_generation_s": round(head["host_generation_s"], 2),
+            "rank_draws": head["rank_draws"], "rank_draw_budget": head["rank_draw_budget"],
         }
         if world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, value)
+            out["cpu_baseline"] = cpu_baseline(args, head["value"], bchk)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

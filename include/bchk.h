@@ -114,6 +114,21 @@ int bchk_count_device(bchk_ctx *ctx, const uint8_t *d_tx, const uint8_t *d_res,
  * may be NULL) is the engine state: pass 0 to start from `seed`. Host-side, sequential. */
 int bchk_generate_host(const bchk_ctx *ctx, double snr_db, size_t B, uint64_t *rng_state,
                        uint64_t seed, uint8_t *tx, double *y);
+/* As above, and draws = the engine draws the B words consumed. */
+int bchk_generate_host_draws(const bchk_ctx *ctx, double snr_db, size_t B, uint64_t *rng_state,
+                             uint64_t seed, uint8_t *tx, double *y, uint64_t *draws);
+/* The engine state `draws` draws after `state` (minstd_rand0: state * 16807^draws mod
+ * 2^31 - 1; a seed is a state): disjoint ranges of the one reference stream per rank or
+ * process. */
+uint64_t bchk_rng_jump(uint64_t state, uint64_t draws);
+/* One block of a (sharded) fun() sweep (src/dataForPlot.cpp:41-74): from engine state
+ * *rng_state (in/out), `skip` words are generated and dropped (the blocks of other ranks),
+ * then B words are generated at Eb/N0 snr_db and decoded on the GPU:
+ *   tx [B][n], res [B][n] (zero where not accepted), accepted [B], ops [B][3] = decodes,
+ *   comparisons, sums, states [B] = engine state after word b (where a sweep resumes when
+ *   it stops after word b). */
+int bchk_sweep_block(bchk_ctx *ctx, double snr_db, uint64_t *rng_state, size_t skip, size_t B,
+                     uint8_t *tx, uint8_t *res, uint8_t *accepted, uint64_t *ops, uint64_t *states);
 
 /* fun(file, decoder, g, gSize, p, e, maxSTNR) (headers/dataForPlot.h:8,
  * src/dataForPlot.cpp:16-116) on the GPU: identical CSV text, written to csv (cap bytes,

@@ -420,3 +420,53 @@ long orc_sweep(const orc_code *c, double decoder_snr_db, int J, long p, long e,
     }
     return off;
 }
+
+/* ------------------------------------------------------- stream helpers (tests) */
+uint64_t orc_stream_draws(const orc_code *c, uint64_t *state, long count, double snr_db) {
+    /* counts minstd() calls by re-deriving them: the engine is x <- 16807 x mod (2^31 - 1),
+     * so the draws between two states are found by stepping a copy alongside */
+    orc_rng r = {*state}, probe;
+    unsigned char info[ORC_MAXN + 1], tx[ORC_MAXN + 1];
+    double y[ORC_MAXN + 1];
+    const double sd = orc_sigma(c, snr_db);
+    uint64_t draws = 0;
+    for (long w = 0; w < count; ++w) {
+        probe = r;
+        orc_gen_info(&r, info, c->k);            /* bchCoder.cpp:236-240 */
+        orc_encode(c, info, tx);
+        orc_add_noise(&r, sd, tx, y, c->n);      /* bchCoder.cpp:243-250 */
+        while (probe.x != r.x) {                 /* the draws this word consumed */
+            probe.x = (probe.x * 16807u) % 2147483647u;
+            ++draws;
+        }
+    }
+    *state = r.x;
+    return draws;
+}
+
+void orc_sweep_block(const orc_code *c, double decoder_snr_db, int J, double snr_db, uint64_t *state,
+                     long skip, long B, unsigned char *tx, unsigned char *res, unsigned char *acc,
+                     uint64_t *ops, uint64_t *states) {
+    orc_rng r = {*state};
+    unsigned char info[ORC_MAXN + 1], junk[ORC_MAXN + 1];
+    double y[ORC_MAXN + 1];
+    const double sd = orc_sigma(c, snr_db), s2 = pow(orc_sigma(c, decoder_snr_db), 2);
+    const int n = c->n;
+    for (long w = 0; w < skip + B; ++w) {
+        unsigned char *row = w < skip ? junk : tx + (w - skip) * n;
+        orc_gen_info(&r, info, c->k);            /* dataForPlot.cpp:47-50 */
+        orc_encode(c, info, row);
+        orc_add_noise(&r, sd, row, y, n);
+        if (w < skip) continue;
+        const long b = w - skip;
+        orc_stats st;
+        memset(res + b * n, 0, (size_t)n);
+        orc_kaneko_decode(c, s2, J, y, res + b * n, NULL, &st);  /* :52 */
+        acc[b] = (unsigned char)st.accepted;
+        ops[3 * b] = st.decodes;
+        ops[3 * b + 1] = st.cmp;
+        ops[3 * b + 2] = st.sum;
+        states[b] = r.x;
+    }
+    *state = r.x;
+}

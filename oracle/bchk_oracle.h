@@ -65,6 +65,16 @@ void orc_kaneko_decode(const orc_code *c, double s2, int J, const double *y,
 
 /* Monte-Carlo FER sweep fun(), src/dataForPlot.cpp:16-116, into a text buffer
  * (CSV). Returns the number of bytes written (or -1 if cap is too small). */
+/* Engine draws of `count` stream words from state *state (advanced), at Eb/N0 snr_db:
+ * the words of src/dataForPlot.cpp:47-50 (generateRandomPoly + addNoise). */
+uint64_t orc_stream_draws(const orc_code *c, uint64_t *state, long count, double snr_db);
+/* One block of fun()'s loop body (src/dataForPlot.cpp:47-53): from engine state *state
+ * (advanced), `skip` words dropped, then B words generated and decoded (res rows zeroed first,
+ * written on acceptance): tx, res [B][n], acc [B], ops [B][3] = decodes/cmp/sums, states [B]
+ * = the engine state after each word. */
+void orc_sweep_block(const orc_code *c, double decoder_snr_db, int J, double snr_db, uint64_t *state,
+                     long skip, long B, unsigned char *tx, unsigned char *res, unsigned char *acc,
+                     uint64_t *ops, uint64_t *states);
 long orc_sweep(const orc_code *c, double decoder_snr_db, int J, long p, long e,
                double max_snr, uint64_t seed, char *out, long cap);
 

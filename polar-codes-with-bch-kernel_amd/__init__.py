@@ -31,7 +31,7 @@ EXPORTS = (
     "bchk_create", "bchk_destroy", "bchk_code_params", "bchk_generator",
     "bchk_set_max_decodes", "bchk_decode_host", "bchk_decode_device",
     "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device",
-    "bchk_generate_host", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
+    "bchk_generate_host", "bchk_generate_host_draws", "bchk_rng_jump", "bchk_sweep_block", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
     "bchk_profile_read", "bchk_profile_read_stages", "bchk_path_counts", "bchk_tail_count",
     "bchk_tail_stats", "bchk_tail_diag_read", "bchk_set_fast_path", "bchk_set_analytic",
     "bchk_set_chunk_limit", "bchk_set_syndrome_table",
@@ -87,6 +87,10 @@ def lib():
     L.bchk_alg_decode_host.argtypes = [vp, vp, vp, sz, vp, vp]
     L.bchk_count_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
     L.bchk_generate_host.argtypes = [vp, dbl, sz, C.POINTER(u64), u64, vp, vp]
+    L.bchk_generate_host_draws.argtypes = [vp, dbl, sz, C.POINTER(u64), u64, vp, vp, C.POINTER(u64)]
+    L.bchk_rng_jump.argtypes = [u64, u64]
+    L.bchk_rng_jump.restype = u64
+    L.bchk_sweep_block.argtypes = [vp, dbl, C.POINTER(u64), sz, sz, vp, vp, vp, vp, vp]
     L.bchk_sweep.argtypes = [vp, C.c_long, C.c_long, dbl, C.POINTER(u64), u64, sz, C.c_char_p, sz]
     L.bchk_sync.argtypes = [vp]
     L.bchk_stream.argtypes = [vp]
@@ -208,6 +212,28 @@ class KanekoKernelProcessor:
         st = C.c_uint64(state)
         _check(lib().bchk_generate_host(self._h, snr_db, B, C.byref(st), seed, _p(tx), _p(y)))
         return tx, y, st.value
+
+    def generate_draws(self, snr_db, B, seed=1, state=0):
+        """generate() and the engine draws it consumed: (tx, y, next_state, draws)."""
+        tx = np.zeros((B, self.n), np.uint8)
+        y = np.zeros((B, self.n), np.float64)
+        st, dr = C.c_uint64(state), C.c_uint64()
+        _check(lib().bchk_generate_host_draws(self._h, snr_db, B, C.byref(st), seed, _p(tx), _p(y),
+                                              C.byref(dr)))
+        return tx, y, st.value, dr.value
+
+    def sweep_block(self, snr_db, state, skip, B):
+        """One block of a sharded fun() sweep (bchk_sweep_block): (tx, res, accepted,
+        ops [B, 3] = decodes/comparisons/sums, states [B] after each word, state after)."""
+        tx = np.zeros((B, self.n), np.uint8)
+        res = np.zeros((B, self.n), np.uint8)
+        acc = np.zeros(B, np.uint8)
+        ops = np.zeros((B, 3), np.uint64)
+        states = np.zeros(B, np.uint64)
+        st = C.c_uint64(state)
+        _check(lib().bchk_sweep_block(self._h, snr_db, C.byref(st), skip, B, _p(tx), _p(res), _p(acc),
+                                      _p(ops), _p(states)))
+        return tx, res, acc, ops, states, st.value
 
     def sweep(self, p, e, max_snr=5.0, seed=1, batch=0, state=0, return_state=False):
         """fun() on the GPU: the reference CSV text (and the engine state after it)."""
@@ -341,6 +367,14 @@ class PolarListDecoder:
         _check(lib().bchk_polar_sync(self._h))
 
 
+def rng_jump(state, draws):
+    """The reference engine's state `draws` draws after `state` (a seed is a state)."""
+    return int(lib().bchk_rng_jump(int(state), int(draws)))
+
+
+MINSTD_PERIOD = 2147483646  # minstd_rand0: 2^31 - 2
+
+
 def syndrome_table_query(m, t, syndromes):
     """Host-side Decoder::decode through the syndrome table (no GPU): syndromes [N][t] odd
     syndromes S_1, S_3, ... as uint32 -> (ok [N] bool, flipped-position masks [N] uint64)."""
@@ -361,3 +395,5 @@ def syndrome_table_info(m, t):
 
 def version():
     return lib().bchk_version().decode()
+
+from . import sweep_dist  # noqa: E402,F401  (sharded fun() sweep over ranks)

@@ -818,8 +818,26 @@ int bchk_count_device(bchk_ctx *c, const uint8_t *d_tx, const uint8_t *d_res, co
 // The reference's stream: std::default_random_engine (seed 1 unless RANDOM is defined,
 // src/bchCoder.cpp:14-22), uniform_int_distribution<unsigned short>(0, 1) for the
 // information bits and a fresh normal_distribution(0, sd) per addNoise call.
-static void gen_word(std::default_random_engine &eng, const bchk_ctx *c, double sd, uint8_t *tx,
-                     double *y, std::vector<uint8_t> &info) {
+}  // extern "C"
+
+// The reference's engine with a count of its draws (the distributions see the same
+// result_type, min, max and values, so the stream is unchanged).
+struct CountingEngine {
+    using Eng = std::default_random_engine;
+    using result_type = Eng::result_type;
+    Eng &e;
+    uint64_t n = 0;
+    static constexpr result_type min() { return Eng::min(); }
+    static constexpr result_type max() { return Eng::max(); }
+    result_type operator()() {
+        ++n;
+        return e();
+    }
+};
+
+template <class Eng>
+static void gen_word(Eng &eng, const bchk_ctx *c, double sd, uint8_t *tx, double *y,
+                     std::vector<uint8_t> &info) {
     std::uniform_int_distribution<unsigned short> bit(0, 1);
     for (int i = 0; i < c->k; ++i) info[i] = (uint8_t)bit(eng);
     memset(tx, 0, c->n);
@@ -830,10 +848,78 @@ static void gen_word(std::default_random_engine &eng, const bchk_ctx *c, double 
     for (int i = 0; i < c->n; ++i) y[i] = (tx[i] ? 1 : -1) + noise(eng);
 }
 
+extern "C" {
+
 static double sweep_sigma(const bchk_ctx *c, double stnr) {
     // src/dataForPlot.cpp:45 (getK()/getN() return long)
     const long K = c->k, Nn = c->n;
     return sqrt(1 / (pow(10, stnr / 10) * 2 * K / Nn));
+}
+
+// minstd_rand0: x <- 16807 x mod (2^31 - 1); jumping d draws ahead multiplies by 16807^d.
+static constexpr uint64_t kMinstdM = 2147483647ull, kMinstdA = 16807ull;
+static uint64_t minstd_state(uint64_t s) {  // the state std::minstd_rand0(s) starts from
+    s %= kMinstdM;
+    return s ? s : 1ull;
+}
+
+uint64_t bchk_rng_jump(uint64_t state, uint64_t draws) {
+    uint64_t r = minstd_state(state), a = kMinstdA;
+    for (uint64_t e = draws % (kMinstdM - 1); e; e >>= 1) {  // period 2^31 - 2
+        if (e & 1) r = r * a % kMinstdM;
+        a = a * a % kMinstdM;
+    }
+    return r;
+}
+
+int bchk_generate_host_draws(const bchk_ctx *c, double snr_db, size_t B, uint64_t *rng_state, uint64_t seed,
+                             uint8_t *tx, double *y, uint64_t *draws) {
+    if (!c || (B && (!tx || !y))) return fail(BCHK_EINVAL, "NULL argument");
+    std::default_random_engine eng(minstd_state(rng_state && *rng_state ? *rng_state : seed));
+    CountingEngine ce{eng};
+    std::vector<uint8_t> info(c->k);
+    const double sd = sweep_sigma(c, snr_db);
+    for (size_t b = 0; b < B; ++b) gen_word(ce, c, sd, tx + b * c->n, y + b * c->n, info);
+    if (rng_state) {
+        std::stringstream ss;
+        ss << eng;
+        ss >> *rng_state;
+    }
+    if (draws) *draws = ce.n;
+    return 0;
+}
+
+int bchk_sweep_block(bchk_ctx *c, double snr_db, uint64_t *rng_state, size_t skip, size_t B, uint8_t *tx,
+                     uint8_t *res, uint8_t *accepted, uint64_t *ops, uint64_t *states) {
+    if (!c || !rng_state || (B && (!tx || !res || !accepted || !ops || !states)))
+        return fail(BCHK_EINVAL, "NULL argument");
+    std::default_random_engine eng(minstd_state(*rng_state));
+    std::vector<uint8_t> info(c->k), junk(c->n);
+    std::vector<double> yj(c->n), y(B * c->n);
+    const double sd = sweep_sigma(c, snr_db);
+    for (size_t b = 0; b < skip; ++b) gen_word(eng, c, sd, junk.data(), yj.data(), info);
+    for (size_t b = 0; b < B; ++b) {
+        gen_word(eng, c, sd, tx + b * c->n, y.data() + b * c->n, info);
+        std::stringstream ss;
+        ss << eng;
+        ss >> states[b];
+    }
+    {
+        std::stringstream ss;
+        ss << eng;
+        ss >> *rng_state;
+    }
+    if (B == 0) return 0;
+    std::vector<bchk_stats> st(B);
+    memset(res, 0, B * c->n);
+    if (int rc = bchk_decode_host(c, y.data(), B, res, nullptr, st.data())) return rc;
+    for (size_t b = 0; b < B; ++b) {
+        accepted[b] = (st[b].flags & BCHK_F_ACCEPTED) ? 1 : 0;
+        ops[3 * b] = st[b].decodes;
+        ops[3 * b + 1] = st[b].comparisons;
+        ops[3 * b + 2] = st[b].sums;
+    }
+    return 0;
 }
 
 int bchk_generate_host(const bchk_ctx *c, double snr_db, size_t B, uint64_t *rng_state, uint64_t seed,

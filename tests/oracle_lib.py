@@ -52,6 +52,11 @@ def lib():
         L.orc_gen_info.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         L.orc_encode.argtypes = [P(OrcCode), C.c_void_p, C.c_void_p]
         L.orc_add_noise.argtypes = [C.c_void_p, C.c_double, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_stream_draws.argtypes = [P(OrcCode), C.POINTER(C.c_uint64), C.c_long, C.c_double]
+        L.orc_stream_draws.restype = C.c_uint64
+        L.orc_sweep_block.argtypes = [P(OrcCode), C.c_double, C.c_int, C.c_double, C.POINTER(C.c_uint64),
+                                      C.c_long, C.c_long, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p]
         _lib = L
     return _lib
 
@@ -114,6 +119,25 @@ class Oracle:
                             buf, len(buf))
         assert r >= 0
         return buf.raw[:r].decode()
+
+    def stream_draws(self, state, count, snr_db):
+        """(engine draws of `count` stream words from `state`, the state after them)."""
+        st = C.c_uint64(state)
+        d = lib().orc_stream_draws(C.byref(self.code), C.byref(st), count, snr_db)
+        return int(d), st.value
+
+    def sweep_block(self, J, snr_db, state, skip, B, decoder_snr_db=0.5):
+        """fun()'s loop body over one block (orc_sweep_block): the block source of
+        sweep_dist.sharded_sweep."""
+        tx = np.zeros((B, self.n), np.uint8)
+        res = np.zeros((B, self.n), np.uint8)
+        acc = np.zeros(B, np.uint8)
+        ops = np.zeros((B, 3), np.uint64)
+        states = np.zeros(B, np.uint64)
+        st = C.c_uint64(state)
+        lib().orc_sweep_block(C.byref(self.code), decoder_snr_db, J, snr_db, C.byref(st), skip, B,
+                              _p(tx), _p(res), _p(acc), _p(ops), _p(states))
+        return tx, res, acc, ops, states, st.value
 
     def stream(self, seed, count, snr_db):
         """The reference's fun() input stream: (tx [count,n], y [count,n])."""

@@ -1,6 +1,12 @@
-"""The N > 1 path of bench.py on CPU: world_size-2 gloo processes run the same per-step
-counter exchange and max-over-ranks timing the GPU run uses over RCCL, and each rank's
-input stream is disjoint from the others (weak scaling, no data-path collective)."""
+"""The N > 1 paths on CPU (world_size-2 gloo processes) and, under -m gpu, with both ranks on
+device 0:
+  * bench.py's per-step counter exchange and max-over-ranks timing (RCCL on the GPU run);
+  * the ranks' input streams: disjoint jump-ahead ranges of the one reference stream,
+    checked over every draw a rank consumes;
+  * the sharded FER sweep (polar-codes-with-bch-kernel_amd/sweep_dist.py): blocks of the
+    stream per rank, one all-gather + one all-reduce per round, the e-error stop cut in
+    stream order -- its CSV is byte-identical to the reference's fun() output."""
+import hashlib
 import os
 import socket
 
@@ -11,7 +17,11 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import bench
+from bchk_pkg import load
+from golden import sweep_files
 from oracle_lib import Oracle
+
+PERIOD = 2147483646  # minstd_rand0
 
 
 def _free_port():
@@ -22,7 +32,21 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _run(world, target, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda x: x[0])
+
+
+def _counter_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     # rank r decodes its own stream: here its counters are synthetic but rank-specific
@@ -37,25 +61,135 @@ def _worker(rank, world, port, q):
 
 
 def test_counter_exchange_and_max_timing_world2():
-    world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    for rank, total, el in out:
+    for rank, total, el in _run(2, _counter_worker):
         # 3 steps x sum over ranks, never re-reducing the running total
         assert total == [3 * 3, 3 * 30, 2 * (100 + 101 + 102), 3 * 14, 3 * 10, 3 * 2000]
         assert el == 1.5
 
 
-def test_rank_streams_are_disjoint():
+def test_rng_jump_is_the_engine_stepped():
+    F = load()
+    for seed in (1, 12345, PERIOD):
+        x = seed % 2147483647 or 1
+        for d in range(1, 2000):
+            x = x * 16807 % 2147483647
+            if d in (1, 2, 17, 1999):
+                assert F.rng_jump(seed, d) == x
+        a, b = 123456789, 987654321
+        assert F.rng_jump(F.rng_jump(seed, a), b) == F.rng_jump(seed, a + b)
+        assert F.rng_jump(seed, PERIOD) == (seed % 2147483647 or 1)
+
+
+def test_rank_streams_are_disjoint_over_every_draw():
+    # rank r starts D = period / world draws after rank r - 1 and must use at most D draws:
+    # its range [r D, r D + used) then never meets another rank's. The draw count is the
+    # engine's own (the oracle steps a copy of the state), checked against the jump.
+    F = load()
     o = Oracle(6, 6)
-    _, y0 = o.stream(bench.rank_seed(1, 0), 64, 5.0)
-    _, y1 = o.stream(bench.rank_seed(1, 1), 64, 5.0)
-    assert not np.any(np.all(y0[:, None, :] == y1[None, :, :], axis=2))
+    world = 8
+    starts = []
+    for r in range(world):
+        start, D = bench.rank_stream_start(F, 1, r, world)
+        assert D == PERIOD // world
+        starts.append(start)
+        used, end = o.stream_draws(start, 512, 5.0)
+        assert 0 < used <= D
+        assert F.rng_jump(start, used) == end
+        bench.check_rank_draws(used, D, world)
+    assert len(set(starts)) == world
+    # the full headline batch per rank fits the 8-rank budget (~190 draws per codeword)
+    used, _ = o.stream_draws(starts[0], 1 << 20, 5.0)
+    assert used <= PERIOD // world
+    with pytest.raises(SystemExit):
+        bench.check_rank_draws(PERIOD // world + 1, PERIOD // world, world)
+    # the jump reproduces the stream itself: rank 1's first word is word w of the stream
+    # exactly when w words use rank 1's offset (here: a short stream, offset = its draws)
+    used, _ = o.stream_draws(1, 37, 5.0)
+    tx0, y0 = o.stream(1, 38, 5.0)
+    tx1, y1 = o.stream(F.rng_jump(1, used), 1, 5.0)
+    np.testing.assert_array_equal(y1[0].view(np.uint64), y0[37].view(np.uint64))
+
+
+class OracleSource:
+    """The C oracle's fun() loop body (test infrastructure) as a sweep block source."""
+
+    def __init__(self, m, t, J):
+        self.o, self.J = Oracle(m, t), J
+
+    def block(self, snr, state, skip, B):
+        return self.o.sweep_block(self.J, snr, state, skip, B)
+
+
+def _sweep_worker(rank, world, port, q, m, t, J, p, e, block):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sd = load().sweep_dist
+    csv = sd.sharded_sweep(OracleSource(m, t, J), (1 << m) - 1, p, e, dist=dist, world=world, rank=rank,
+                           block=block)
+    q.put((rank, csv))
+    dist.destroy_process_group()
+
+
+def _golden(name):
+    path = [f for f in sweep_files() if os.path.basename(f) == name][0]
+    return open(path).read()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_sweep_equals_reference_csv_cpu(world):
+    # BCH(15,7,5), J = inf, p = 10^4, e = 10^4 (the reference binary's CSV): small blocks so
+    # every Eb/N0 point spans several rounds and the stop falls inside a rank's block
+    want = _golden("sweep_m4t2_p10000_e10000.csv")
+    if world == 1:
+        sd = load().sweep_dist
+        assert sd.sharded_sweep(OracleSource(4, 2, -1), 15, 10000, 10000, block=700) == want
+        return
+    for _, csv in _run(world, _sweep_worker, 4, 2, -1, 10000, 10000, 700):
+        assert csv == want
+
+
+def test_sharded_sweep_error_cut_world2_cpu():
+    # BCH(31,16,7), J = inf, p = 10^4, e = 100: the e-th frame error ends most points
+    want = _golden("sweep_m5t3_p10000_e100.csv")
+    for _, csv in _run(2, _sweep_worker, 5, 3, -1, 10000, 100, 300):
+        assert csv == want
+
+
+class GpuSource:
+    def __init__(self, m, t, J):
+        self.d = load().KanekoKernelProcessor(m, t, J=J, device=0)
+
+    def block(self, snr, state, skip, B):
+        return self.d.sweep_block(snr, state, skip, B)
+
+
+def _gpu_sweep_worker(rank, world, port, q, m, t, J, p, e, block):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    src = GpuSource(m, t, J)
+    csv = load().sweep_dist.sharded_sweep(src, (1 << m) - 1, p, e, dist=dist, world=world, rank=rank,
+                                          block=block)
+    single = src.d.sweep(p, e) if rank == 0 else None
+    q.put((rank, csv, single))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["sweep_m4t2_p10000_e10000.csv", "sweep_m5t3_p10000_e100.csv"])
+def test_sharded_gpu_sweep_world2_equals_reference_csv(name):
+    m, t = (4, 2) if "m4t2" in name else (5, 3)
+    p, e = (10000, 10000) if "m4t2" in name else (10000, 100)
+    want = _golden(name)
+    out = _run(2, _gpu_sweep_worker, m, t, -1, p, e, 1 << 12)
+    for rank, csv, single in out:
+        assert csv == want
+    assert out[0][2] == want  # the single-GPU bchk_sweep agrees
+
+
+@pytest.mark.gpu
+def test_sharded_gpu_sweep_world2_bch31_j15_pinned_md5():
+    # reference BCH(31,16,7), J = 15, p = 10^6, e = 100 (SURVEY.md §6.4 md5)
+    out = _run(2, _gpu_sweep_worker, 5, 3, 15, 1000000, 100, 1 << 16)
+    for rank, csv, single in out:
+        assert hashlib.md5(csv.encode()).hexdigest() == "105c77e4bb47a243054121d9c907feae"
+    assert out[0][2] == out[0][1]
