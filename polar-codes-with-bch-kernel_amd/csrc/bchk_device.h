@@ -31,6 +31,15 @@ struct TableDesc {
     int32_t EW;  // unused (kept for the struct layout)
 };
 
+// A codeword's search state where the exact first pass hands it to the analytic tail
+// kernel, which resumes from it (no exact chunk decoded twice).
+struct TailRec {
+    double l0;
+    uint64_t bound, jsteps, impr, best;
+    int32_t T, m0;
+    uint32_t chunks, flags;  // flags: 1 firstOK, 2 accepted
+};
+
 struct SearchParams {
     const double *y;       // [B][n]
     uint8_t *res;          // [B][n]
@@ -86,6 +95,18 @@ struct SearchParams {
     // diagnostics: per codeword through the analytic tail, 8 u64 (codeword, cycles of prep,
     // exact chunks, plan, enumeration steps, mode | why << 8 | split chunks << 16, cycles
     // after the plan, decodes); null = off
+    // first pass -> analytic tail: the state of each hand-off, by its queue slot (null = the
+    // tail kernel starts codewords from scratch)
+    TailRec *tail_rec;
+    // the analytic tail kernel's input when it runs concurrently with the first pass (null:
+    // the static queue/qcount above): slots in_queue[k] (kEmptySlot until stored), the
+    // producer's tail, this kernel's ticket counter, the producer's 8 per-XCD done counts
+    // and their final total (null: count)
+    uint32_t *in_queue;
+    const uint32_t *in_tail;
+    uint32_t *in_head;
+    const uint32_t *in_done;
+    const uint32_t *in_total;
     unsigned long long *tail_diag;
     uint32_t *tail_diag_count;
     uint32_t tail_diag_cap;

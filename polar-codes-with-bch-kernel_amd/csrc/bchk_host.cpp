@@ -377,7 +377,7 @@ struct bchk_ctx {
     hipStream_t stream = nullptr;
     size_t lds = 0, lds_alg = 0, lds_tail = 0;
     int grid = 0, grid_tab = 0, grid_tail = 0, grid_tail_tab = 0;
-    DevBuf l1q;  // first pass -> analytic tail kernel
+    DevBuf l1q, l1rec;  // first pass -> analytic tail kernel: codewords, their states
     uint64_t max_decodes = 0;
     DevBuf y, res, l0, st, words, synd, ok;
     // the cooperative kernel runs on `aux`, concurrently with the exact kernel
@@ -388,6 +388,8 @@ struct bchk_ctx {
     uint64_t last_tail = 0;        // codewords the last call handed to the tail kernel
     uint64_t last_tail_stats[6] = {0, 0, 0, 0, 0, 0};
     bool tail_diag_on = false;     // BCHK_TAIL_DIAG=1: per-codeword tail timing records
+    bool tail_concurrent = false;  // BCHK_TAIL_CONCURRENT=1: the tail kernel beside the first pass
+    int tail_conc_blocks = 256;    // blocks of the concurrent tail kernel (one per CU)
     DevBuf tdiag;
     bool profile = false;
     // syndrome decoding table (bchk_syndtab.h): built on first use, shared across contexts
@@ -510,7 +512,13 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     // analytic tail: the first pass hands its heavy codewords to the tail kernel (queue
     // l1q), which finishes most of them and hands the rest to the cooperative kernel
     const bool tail = c->analytic && c->ks.tail && p.heavy_tail && variant == BCHK_VARIANT_ANSWER;
-    if (tail && (rc = c->l1q.ensure(B * sizeof(uint32_t)))) return rc;
+    if (tail && (rc = c->l1rec.ensure(B * sizeof(TailRec)))) return rc;
+    if (tail && B > c->l1q.cap / sizeof(uint32_t)) {
+        if ((rc = c->l1q.ensure(B * sizeof(uint32_t)))) return rc;
+        HIP_TRY(hipMemset(c->l1q.p, 0xFF, c->l1q.cap));  // empty slots (consumers restore them)
+    }
+    // the tail kernel runs on the auxiliary stream, concurrently with the first pass
+    const bool tconc = tail && c->tail_concurrent;
     const bool conc = c->coop_concurrent && p.heavy_tail && !tail;
     hipStream_t cs = conc ? c->aux : s;  // the cooperative kernel's stream
     bchk_ctx::Ev ev{};
@@ -529,9 +537,9 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         HIP_TRY(c->fast(f, c->lds_fast, s));
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[1], s));
-    if (conc) {
+    if (conc || tconc) {
         HIP_TRY(hipEventRecord(c->ev_fork, s));
-        HIP_TRY(hipStreamWaitEvent(cs, c->ev_fork, 0));
+        HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[2], s));
     {
@@ -540,6 +548,7 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
             q.heavy_queue = (uint32_t *)c->l1q.p;
             q.heavy_tail = ctrl + kL1Tail;
             q.heavy_big = 0;
+            q.tail_rec = tconc ? nullptr : (TailRec *)c->l1rec.p;
         }
         if (fast) {
             q.queue = (const uint32_t *)c->queue.p;
@@ -554,7 +563,8 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[3], s));
     SearchParams pc = p;  // the cooperative kernel's view of its producer
-    if (c->profile) HIP_TRY(hipEventRecord(ev.e[6], s));
+    hipStream_t ts = tconc ? c->aux : s;  // the tail kernel's stream
+    if (c->profile) HIP_TRY(hipEventRecord(ev.e[6], ts));
     if (tail) {
         SearchParams q = p;
         q.queue = (const uint32_t *)c->l1q.p;
@@ -563,6 +573,15 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         q.exact_done = ctrl + kTailDone;
         q.analytic = 1;
         q.tail_stats = ctrl + kTailStats;
+        q.tail_rec = (TailRec *)c->l1rec.p;
+        if (tconc) {  // take the first pass's hand-offs as they come; recompute their state
+            q.tail_rec = nullptr;
+            q.in_queue = (uint32_t *)c->l1q.p;
+            q.in_tail = ctrl + kL1Tail;
+            q.in_head = ctrl + kTailHeads;
+            q.in_done = ctrl + kExactDone;
+            q.in_total = fast ? ctrl : nullptr;
+        }
         if (c->tail_diag_on) {
             if (!c->tdiag.p && (rc = c->tdiag.ensure(size_t(1) << 22))) return rc;
             HIP_TRY(hipMemsetAsync(c->tdiag.p, 0, c->tdiag.cap, s));
@@ -570,11 +589,17 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
             q.tail_diag_count = ctrl + kTailStats + 16;
             q.tail_diag_cap = (uint32_t)(c->tdiag.cap / 64);
         }
-        HIP_TRY(launch_tail(c->ks, q, tabk ? c->grid_tail_tab : c->grid_tail, c->lds_tail, s));
+        int tgrid = tabk ? c->grid_tail_tab : c->grid_tail;
+        if (tconc) tgrid = std::min(tgrid, c->tail_conc_blocks);  // leave the first pass its CUs
+        HIP_TRY(launch_tail(c->ks, q, tgrid, c->lds_tail, ts));
         pc.exact_done = ctrl + kTailDone;
         pc.exact_total = ctrl + kL1Tail;
     }
-    if (c->profile) HIP_TRY(hipEventRecord(ev.e[7], s));
+    if (c->profile) HIP_TRY(hipEventRecord(ev.e[7], ts));
+    if (tconc) {  // the cooperative kernel (stream s) follows both
+        HIP_TRY(hipEventRecord(c->ev_join, c->aux));
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    }
     if (p.heavy_tail) {
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));
         HIP_TRY(launch_coop(c->ks, pc, grid_coop, c->lds_coop, cs));
@@ -658,6 +683,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (const char *cc = getenv("BCHK_COOP_CONCURRENT")) c->coop_concurrent = atoi(cc) != 0;
     if (getenv("BCHK_NO_ANALYTIC")) c->analytic = false;
     if (getenv("BCHK_TAIL_DIAG")) c->tail_diag_on = true;
+    if (const char *tc = getenv("BCHK_TAIL_CONCURRENT")) c->tail_concurrent = atoi(tc) != 0;
+    if (const char *tb = getenv("BCHK_TAIL_BLOCKS")) c->tail_conc_blocks = std::max(1, atoi(tb));
     c->lds_coop = tb + c->ks.coop_bytes;
     // one cooperative workgroup per CU by default (LDS sized past half the CU's 160 KB):
     // a heavy codeword's 16 waves then own the CU's four SIMDs, which shortens the longest
@@ -695,6 +722,7 @@ void bchk_destroy(bchk_ctx *c) {
         for (auto &x : e.e) (void)hipEventDestroy(x);
     c->queue.release();
     c->l1q.release();
+    c->l1rec.release();
     c->tdiag.release();
     c->heavy.release();
     c->ctrl.release();

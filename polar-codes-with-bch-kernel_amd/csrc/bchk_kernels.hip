@@ -576,32 +576,50 @@ __device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const
 // (chunks, as before), and from i* on every improvement has l < l0 <= lim, so it is among
 // the enumerated candidates. Nothing fits (stack, candidate list, kernel dimension,
 // budget): the codeword is handed to the cooperative kernel as before.
-constexpr int kAnStack = 256;            // pending nodes of the enumeration
-constexpr int kAnCand = 64;              // candidate codewords kept for the replay
+constexpr int kAnStack = 448;            // pending nodes of the enumeration (64 lanes x depth)
+constexpr int kAnCand = 128;             // candidate codewords kept for the replay
 constexpr int kAnKern = 3;               // kernel dimension of R's columns (2^3 combinations)
 constexpr uint32_t kAnBudget = 4096;     // enumeration nodes per attempt
 constexpr uint32_t kAnExactChunks = 32;  // exact chunks below the split pattern
 constexpr int kAnMaxU = 32;              // |U| <= 32 (n = 63 with NB = 31)
 
 struct AnNode {  // enumeration node: D_U = sel (bits over U indices)
-    uint64_t rem, pos;  // residual syndrome (zero: a codeword), D_U positions
+    uint64_t rem;       // residual syndrome (zero: a codeword)
     int64_t sum;        // sum of a over D_U, fixed point (a lower bound)
     uint32_t sel, comb; // U indices; pattern bits of D_R for this D_U
+    uint32_t next, pad; // the next child to generate
 };
 struct AnCand {
     uint64_t D;  // yH ^ c (positions)
     double l;    // calcL(c), index order
     uint32_t i, m;
 };
+struct AnPend {  // a codeword met by the enumeration, emitted in batches of 64
+    uint32_t sel, comb;
+    int64_t usum;
+};
+constexpr int kAnPend = 128;
 struct AnWave {
     AnNode stack[kAnStack];
     AnCand cand[kAnCand];
+    AnPend pend[kAnPend];
+    // pattern bits -> positions and fixed-point reliability sums, per nibble of D_R; U
+    // indices -> positions, per nibble of sel
+    uint64_t dpos[128];
+    int64_t dsum[128];
+    uint64_t upos[128];
     int64_t afix[kAnMaxU + 1];  // a of U index q, fixed point (2^40), sentinel at NU
     uint64_t ru[kAnMaxU];
     uint32_t cu[kAnMaxU];
     uint32_t kern[kAnKern];
     uint32_t ncand;
     uint8_t pu[kAnMaxU];
+    // residual classes: the residuals all lie in the span of the U columns' residuals and
+    // rem0, identified by their bits at the span's pivot positions (cbits of them): cmask[c]
+    // = the U elements whose residual has class c
+    uint32_t cmask[32];
+    uint8_t cpiv[5];
+    int32_t cbits;
 };
 template <int M, int TMAX>
 constexpr bool an_capable() { return Geo<M>::NW == 1 && TMAX <= 8; }
@@ -621,8 +639,8 @@ __device__ __forceinline__ int64_t an_fix_up(double lim) {
 // pattern, filters (not yet processed exactly, below every possible bound, l < l0), and the
 // candidate list (per lane, divergent).
 template <int TMAX>
-__device__ __forceinline__ void an_emit(AnWave *A, uint64_t pos, uint32_t comb, int wU, int t, int nkern,
-                                        uint64_t ifrom, uint64_t BM, double l0, const uint8_t *ordl,
+__device__ __forceinline__ void an_emit(AnWave *A, uint32_t sel, int64_t usum, uint32_t comb, int wU, int t,
+                                        int nkern, uint64_t ifrom, uint64_t BM, int jb, double l0, double lcap,
                                         const double *ap) {
     for (uint32_t ks = 0; ks < (1u << nkern); ++ks) {
         uint32_t DR = comb;
@@ -630,6 +648,9 @@ __device__ __forceinline__ void an_emit(AnWave *A, uint64_t pos, uint32_t comb, 
         for (int q = 0; q < kAnKern; ++q)
             if (q < nkern && ((ks >> q) & 1u)) DR ^= A->kern[q];
         const int r = t - wU;
+        // more than r bits at or above bit jb stay set after clearing the top r: first
+        // pattern >= 2^jb >= BM (most codewords the enumeration meets at n = 63)
+        if (__popc(DR >> jb) > r) continue;
         uint32_t ifirst;
         if (__popc(DR) <= r) {
             ifirst = (wU == 0 && DR == 0u) ? 1u : 0u;  // c = yH: the hard decision fails
@@ -641,11 +662,18 @@ __device__ __forceinline__ void an_emit(AnWave *A, uint64_t pos, uint32_t comb, 
             ifirst = v;
         }
         if ((uint64_t)ifirst < ifrom || (uint64_t)ifirst >= BM) continue;
-        uint64_t D = pos;
-        for (uint32_t v = DR; v; v &= v - 1) D |= 1ull << ordl[__builtin_ctz(v)];
+        uint64_t D = 0;
+        int64_t lsum = usum;  // fixed-point lower bound of l(c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t v = (DR >> (4 * j)) & 15u, u = (sel >> (4 * j)) & 15u;
+            D |= A->dpos[16 * j + v] | A->upos[16 * j + u];
+            lsum += A->dsum[16 * j + v];
+        }
+        if ((double)lsum * 0x1p-40 > lcap * (1.0 + 0x1p-40)) continue;  // cannot matter
         double l = 0.0;  // calcL (:69-77): index order
         for (uint64_t v = D; v; v &= v - 1) l += ap[__builtin_ctzll(v)];
-        if (!(l < l0)) continue;
+        if (!(l < l0 && l <= lcap)) continue;
         const uint32_t slot = atomicAdd(&A->ncand, 1u);
         if (slot < (uint32_t)kAnCand) {
             AnCand c;
@@ -659,27 +687,34 @@ __device__ __forceinline__ void an_emit(AnWave *A, uint64_t pos, uint32_t comb, 
 }
 
 // Depth-first enumeration of D_U (sum <= limfix, |D_U| <= t) from the root residual. Every
-// lane owns one node whose children it generates, one per step, in ascending order (the
-// first child over the bound ends the node: the reliabilities ascend); children that can
-// have children of their own go on the wave's LDS stack, and lanes without a node take
-// the stack's top entries. So each step visits up to 64 nodes. Returns false when the node
-// budget or the stack runs out (the candidate list is then partial).
+// lane owns one node and generates its children one per step in ascending order (the first
+// child over the bound ends the node: the reliabilities ascend). A child that has children
+// of its own becomes the lane's node, and the parent goes on the wave's LDS stack as a
+// continuation (its next child); lanes without a node take continuations from the top. So
+// each step visits up to 64 nodes, and the stack holds about a descent path per lane.
+// Returns 0, or why the candidate list is partial: 1 node budget, 2 stack, 3 list full.
 template <int TMAX>
-__device__ bool an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t rem0, uint32_t comb0,
-                             int nkern, uint64_t ifrom, uint64_t BM, double l0, const uint8_t *ordl,
+__device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t rem0, uint32_t comb0,
+                             int nkern, uint64_t ifrom, uint64_t BM, double l0, double lcap,
                              const double *ap, uint32_t budget, int lane, uint32_t &iters) {
+    const int jb = BM > 1ull ? 64 - __builtin_clzll(BM - 1ull) : 0;  // patterns < BM: bits < jb
+    const int cbits = A->cbits;
+    int cpiv[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) cpiv[i] = A->cpiv[i];
     if (lane == 0) A->ncand = 0u;
     wave_sync();
-    if (lane == 0 && rem0 == 0ull) an_emit<TMAX>(A, 0ull, comb0, 0, t, nkern, ifrom, BM, l0, ordl, ap);
+    if (lane == 0 && rem0 == 0ull) an_emit<TMAX>(A, 0u, 0, comb0, 0, t, nkern, ifrom, BM, jb, l0, lcap, ap);
     AnNode nd;  // lane 0 starts on the root
     nd.rem = rem0;
-    nd.pos = 0;
     nd.sum = 0;
     nd.sel = 0;
     nd.comb = comb0;
+    nd.next = 0;
+    nd.pad = 0;
     bool have = lane == 0 && t >= 1;
-    int next = 0, sp = 0;
-    uint32_t nodes = 1;
+    int sp = 0, np = 0;  // stack and pending-emission counts
+    uint32_t nodes = 1, steps = 0;
     const uint64_t below = (1ull << lane) - 1ull;
     for (;;) {
         const uint64_t idle = ballot(!have);
@@ -690,44 +725,112 @@ __device__ bool an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t 
             if (k < take) {
                 nd = A->stack[sp - 1 - k];
                 have = true;
-                next = 32 - __builtin_clz(nd.sel);  // stacked nodes are non-empty
             }
         }
         sp -= take;
-        if (ballot(have) == 0ull) break;
+        if (ballot(have) == 0ull) {  // done: emit what is still pending
+            wave_sync();
+            if (lane < np) {
+                const AnPend e = A->pend[lane];
+                an_emit<TMAX>(A, e.sel, e.usum, e.comb, __popc(e.sel), t, nkern, ifrom, BM, jb, l0, lcap, ap);
+            }
+            wave_sync();
+            break;
+        }
         ++iters;
         wave_sync();  // the pops are read before this step's pushes reuse their slots
         const int depth = __popc(nd.sel);
+        const int next = (int)nd.next;
         const int q = next < NU ? next : NU;  // NU: the sentinel (never fits)
-        const bool valid = have && next < NU && depth < t && A->afix[q] <= limfix - nd.sum;
-        have = valid;  // a node ends at its first child over the bound
-        nodes += (uint32_t)__popcll(ballot(valid));
+        const int64_t X = limfix - nd.sum;
+        const bool valid = have && next < NU && depth < t && A->afix[q] <= X;
         const int qc = valid ? q : 0;
-        const int64_t cs = nd.sum + A->afix[qc];
+        const int64_t aq = A->afix[qc];
+        const int64_t anext = A->afix[qc + 1 <= NU ? qc + 1 : NU];
+        const int64_t cs = nd.sum + aq;
+        const bool expand = valid && depth + 1 < t && qc + 1 < NU && anext <= limfix - cs;
+        // no child from q on can expand (the pair sums ascend): all of them are leaves, and
+        // the ones whose residual matches are found from the class masks at once
+        const bool run = valid && !expand && cbits >= 0;
+        const bool single = valid && !run;
+        // a single child (visited one per step)
         const uint64_t crem = nd.rem ^ A->ru[qc];
         const uint32_t ccomb = nd.comb ^ A->cu[qc];
-        const uint64_t cpos = nd.pos | (1ull << A->pu[qc]);
-        if (valid && crem == 0ull)
-            an_emit<TMAX>(A, cpos, ccomb, depth + 1, t, nkern, ifrom, BM, l0, ordl, ap);
-        const bool expand = valid && depth + 1 < t && qc + 1 < NU && A->afix[qc + 1] <= limfix - cs;
-        const uint64_t em = ballot(expand);
+        const uint32_t csel = nd.sel | (1u << qc);
+        // a leaf run from q on: of the remaining children only those whose residual
+        // matches can be codewords; walked in ascending order until one is over the bound
+        uint32_t matches = 0;
+        if (run) {
+            uint32_t cl = 0;
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+                if (i < cbits) cl |= (uint32_t)((nd.rem >> cpiv[i]) & 1ull) << i;
+            matches = A->cmask[cl] & ~((1u << qc) - 1u);
+        }
+        (void)nodes;
+        // codewords (zero residual) that can still reach a pattern below BM wait for the
+        // next batch of emissions (a whole wave processes 64 together)
+        bool pend = single && crem == 0ull && (nkern > 0 || __popc(ccomb >> jb) <= t - depth - 1);
+        uint32_t psel = csel, pcomb = ccomb;
+        int64_t psum = cs;
+        for (;;) {
+            const uint64_t pm = ballot(pend);
+            if (pm == 0ull && ballot(matches != 0u) == 0ull) break;
+            if (pend) {
+                AnPend e;
+                e.sel = psel;
+                e.comb = pcomb;
+                e.usum = psum;
+                A->pend[np + __popcll(pm & below)] = e;
+            }
+            np += __popcll(pm);
+            if (np >= 64) {
+                wave_sync();
+                const AnPend e = A->pend[np - 1 - lane];
+                an_emit<TMAX>(A, e.sel, e.usum, e.comb, __popc(e.sel), t, nkern, ifrom, BM, jb, l0, lcap, ap);
+                np -= 64;
+                wave_sync();
+            }
+            // next match of this lane's leaf run (the run ends at the first one over the bound)
+            pend = false;
+            if (matches) {
+                const int m = __builtin_ctz(matches);
+                matches &= matches - 1u;
+                const int64_t am = A->afix[m];
+                if (am <= X) {
+                    psel = nd.sel | (1u << m);
+                    pcomb = nd.comb ^ A->cu[m];
+                    psum = nd.sum + am;
+                    pend = nkern > 0 || __popc(pcomb >> jb) <= t - depth - 1;
+                } else {
+                    matches = 0;
+                }
+            }
+        }
+        // the parent stays open iff its next child fits too
+        const bool cont = expand && anext <= X;
+        const uint64_t em = ballot(cont);
         const int cnt = __popcll(em);
-        if (sp + cnt > kAnStack) return false;
-        if (expand) {
-            AnNode c;
-            c.rem = crem;
-            c.pos = cpos;
-            c.sum = cs;
-            c.sel = nd.sel | (1u << qc);
-            c.comb = ccomb;
+        if (sp + cnt > kAnStack) return 2;
+        if (cont) {
+            AnNode c = nd;
+            c.next = (uint32_t)(qc + 1);
             A->stack[sp + __popcll(em & below)] = c;
         }
         sp += cnt;
-        ++next;
+        if (expand) {  // descend
+            nd.rem = crem;
+            nd.sum = cs;
+            nd.sel = csel;
+            nd.comb = ccomb;
+        }
+        nd.next = (uint32_t)(qc + 1);
+        const bool valid_next = single;  // a leaf run ends the node
+        have = valid_next;
         wave_sync();
-        if (nodes > budget) return false;
+        if (++steps > budget / 8) return 1;  // the DP bound keeps real enumerations far below
     }
-    return A->ncand <= (uint32_t)kAnCand;
+    return A->ncand <= (uint32_t)kAnCand ? 0 : 3;
 }
 
 // First chunk boundary at or after the earliest candidate with l <= lim (~0 if none): from
@@ -735,9 +838,9 @@ __device__ bool an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t 
 __device__ __forceinline__ uint64_t an_earliest(const AnWave *A, double lim, int lane) {
     const uint32_t nc = A->ncand;
     uint32_t best = 0xFFFFFFFFu;
-    if ((uint32_t)lane < nc) {
-        const AnCand c = A->cand[lane];
-        if (c.l <= lim) best = c.i;
+    for (uint32_t e = (uint32_t)lane; e < nc && e < (uint32_t)kAnCand; e += 64) {
+        const AnCand c = A->cand[e];
+        if (c.l <= lim && c.i < best) best = c.i;
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -751,18 +854,22 @@ struct AnPlan {
     int mode;       // 0: hand off, 1: candidates complete from ifrom, 2: exact below stop
     uint64_t stop;  // mode 2: first pattern the replay takes over (a chunk boundary)
     int why;        // mode 0: 1 geometry, 2 kernel dimension, 3 no split within the
-                    // budget, 4 split too far, 5 re-enumeration failed
+                    // budget, 4 split too far
+    int fails;      // enumeration failures seen: bit 1 budget, 2 stack, 3 candidates
+    uint32_t t_elim, t_setup;  // diagnostics: cycles to the end of the elimination, the setup
+    uint32_t t_cls, t_tab;     // ... the residual classes, the nibble tables
 };
 
 // Plan the rest of the search of one codeword from pattern ifrom (a chunk boundary, every
 // earlier pattern processed exactly); candidates land in A.
 template <int M, int TMAX>
 __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const SearchParams &p,
-                          AnWave *A, const uint32_t *col, const uint8_t *ordl, const double *ap,
-                          uint64_t ifrom, int lane, uint32_t &iters) {
+                          AnWave *A, const uint32_t *col, const uint8_t *ordl, const double *as,
+                          const double *ap, uint64_t ifrom, int lane, uint32_t &iters) {
     constexpr int N = Geo<M>::N, W = Prep<M, TMAX>::W;
     const int t = p.t, J = p.J;
-    AnPlan plan{0, 0, 0};
+    AnPlan plan{0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_0 = p.tail_diag ? __builtin_amdgcn_s_memtime() : 0;
     // NB pattern bits: every pattern any future bound admits, and |U| <= 32
     int NB;
     if (N >= 63) NB = 31;
@@ -786,6 +893,7 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     }
     uint32_t comb = lane < NB ? (1u << lane) : 0u;
     bool used = false;
+    uint64_t pivbits = 0;  // bits that hold a pivot of the flip columns
 #pragma unroll
     for (int q = 0; q < TMAX; ++q) {
         if (q >= t) break;
@@ -795,6 +903,7 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
             const bool has = (v >> bit) & 1ull;
             const uint64_t cm = ballot(has && lane < NB && !used);
             if (!cm) continue;
+            pivbits |= 1ull << bit;
             const int k = (int)__builtin_ctzll(cm);
             const uint64_t pv = rdl64(v, k);
             const uint32_t pc = rdl(comb, k);
@@ -819,6 +928,7 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     }
     const uint64_t rem0 = rdl64(v, N);
     const uint32_t comb0 = rdl(comb, N);
+    if (p.tail_diag) plan.t_elim = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
     if (lane >= NB && lane < N) {
         const int q = lane - NB;
         A->afix[q] = an_fix(P.asv[0]);
@@ -827,47 +937,159 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
         A->pu[q] = (uint8_t)P.ordv[0];
     }
     if (lane == 0) A->afix[NU] = (int64_t)0x7FFFFFFFFFFFFFFFll;
+    // residual classes (leaf runs of the enumeration): a reduced basis of the span of the U
+    // residuals and rem0; a residual's bits at its pivots identify it within the span
+    {
+        uint64_t w = (lane >= NB && lane <= N) ? v : 0ull;
+        bool used2 = false;
+        int cb = 0;
+        int piv[5] = {0, 0, 0, 0, 0};
+        // residuals are zero at the flip pivots: only the other bits can hold a pivot
+        uint64_t cand_bits = 0;
+#pragma unroll
+        for (int q = 0; q < TMAX; ++q)
+            if (q < t) cand_bits |= (uint64_t)((1u << M) - 1u) << (8 * q);
+        cand_bits &= ~pivbits;
+        for (uint64_t bb = cand_bits; bb && cb <= 5; bb &= bb - 1) {  // wave-uniform
+            const int bit = (int)__builtin_ctzll(bb);
+            const bool has = (w >> bit) & 1ull;
+            const uint64_t cm = ballot(has && !used2);
+            if (!cm) continue;
+            const int k = (int)__builtin_ctzll(cm);
+            const uint64_t pv = rdl64(w, k);
+            if (has && lane != k) w ^= pv;
+            used2 = used2 || lane == k;
+            if (cb < 5) piv[cb] = bit;
+            ++cb;
+        }
+        const int cbits = cb <= 5 ? cb : -1;  // too many classes: no leaf runs
+        uint32_t cls = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (i < cbits) cls |= (uint32_t)((v >> piv[i]) & 1ull) << i;
+        if (cbits >= 0) {
+            for (int c = 0; c < (1 << cbits); ++c) {
+                const uint64_t bm = ballot(lane >= NB && lane < N && cls == (uint32_t)c);
+                if (lane == 0) A->cmask[c] = (uint32_t)(bm >> NB);
+            }
+        }
+        if (lane == 0) {
+            A->cbits = cbits;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) A->cpiv[i] = (uint8_t)piv[i];
+        }
+    }
+    if (p.tail_diag) plan.t_cls = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
+    // nibble tables of the flip set: entry 16 j + v covers pattern bits 4 j .. 4 j + 3 set in v
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int e = lane + 64 * h, j = e >> 4, v = e & 15;
+        uint64_t dp = 0;
+        int64_t ds = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int b = 4 * j + k;
+            if (((v >> k) & 1) && b < NB) {
+                dp |= 1ull << ordl[b];
+                ds += an_fix(as[b]);
+            }
+        }
+        A->dpos[e] = dp;
+        A->dsum[e] = ds;
+        uint64_t up = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = 4 * j + k;
+            if (((v >> k) & 1) && q < NU) up |= 1ull << ordl[NB + q];
+        }
+        A->upos[e] = up;
+    }
     wave_sync();
+    if (p.tail_diag) plan.t_tab = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
     const double l0 = S.l0;
     const double full = l0 * (1.0 + 0x1p-40);
-    if (an_enumerate<TMAX>(A, NU, t, an_fix_up(full), rem0, comb0, nkern, ifrom, BM, l0, ordl, ap, kAnBudget,
-                           lane, iters)) {
-        plan.mode = 1;
-        return plan;
+    // No U subset of 3 or more fits under l0: at most 1 + NU + NU (NU - 1) / 2 nodes, so the
+    // complete enumeration goes ahead without counting.
+    if (NU < 3 || t <= 2 ||
+        rdlf(P.asv[0], NB) + rdlf(P.asv[0], NB + 1) + rdlf(P.asv[0], NB + 2) > full) {
+        if (p.tail_diag) plan.t_setup = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
+        const int er = an_enumerate<TMAX>(A, NU, t, an_fix_up(full), rem0, comb0, nkern, ifrom, BM, l0, l0, ap,
+                                          2 * kAnBudget, lane, iters);
+        if (!er) {
+            plan.mode = 1;
+            return plan;
+        }
+        plan.fails |= 1 << er;
     }
-    // tighter bounds lim_k = the sum of the k least reliable U positions, ascending k (the
-    // enumeration grows ~5x per step): the largest k within the budget whose earliest
-    // candidate with l <= lim_k comes first wins; the exact chunks then end at its pattern
-    const int kmax = (t + 1 < NU ? t + 1 : NU);
-    int best_k = 0, cur_k = 0;
-    uint64_t best_stop = 0;
-    double lim = 0.0;
-    for (int k = 1; k <= kmax; ++k) {
-        lim += rdlf(P.asv[0], NB + k - 1);
-        if (!(lim < full)) break;  // no tighter than l0 (that attempt failed)
-        cur_k = k;
-        if (!an_enumerate<TMAX>(A, NU, t, an_fix_up(lim * (1.0 + 0x1p-40)), rem0, comb0, nkern, ifrom, BM, l0,
-                                ordl, ap, kAnBudget, lane, iters))
-            break;
+    // Bound from a count: subsets of U of size <= t by floored bin sum (bins of width
+    // hi / 64, lane = bin; a DP over the ascending reliabilities), an upper bound of the
+    // enumeration's nodes at every bin edge. The largest bound within the budget is taken:
+    // l0 itself when it fits (the candidates are then complete), else a tighter one.
+    double prefix_t = 0.0;  // sum of the t least reliable U positions
+    for (int q = 0; q < t && q < NU; ++q) prefix_t += rdlf(P.asv[0], NB + q);
+    const double hi = full < 2.0 * prefix_t ? full : 2.0 * prefix_t;
+    const double delta = hi / 63.0;  // sums <= hi land in bins 0..63
+    uint32_t dp[TMAX + 1];
+#pragma unroll
+    for (int w = 0; w <= TMAX; ++w) dp[w] = (w == 0 && lane == 0) ? 1u : 0u;
+    // bin of every U element (lane NB + q), all at once
+    int mybin = 64;
+    {
+        const double inv = delta > 0.0 ? 1.0 / delta : 0.0;
+        const double bq = P.asv[0] * inv;
+        if (delta > 0.0 && lane >= NB && lane < N && bq < 64.0) mybin = (int)bq;
+    }
+    for (int q = 0; q < NU; ++q) {
+        const int b = (int)rdl((uint32_t)mybin, NB + q);
+        if (b >= 64) break;  // ascending: no later element fits a bin either
+#pragma unroll
+        for (int w = TMAX; w >= 1; --w) {
+            if (w > t) continue;
+            const uint32_t from = (uint32_t)__shfl((int)dp[w - 1], (lane - b) & 63, 64);
+            const uint32_t add = lane >= b ? from : 0u;
+            dp[w] = dp[w] + add < dp[w] ? 0xFFFFFFFFu : dp[w] + add;  // saturating
+        }
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int w = 0; w <= TMAX; ++w) cnt = cnt + dp[w] < cnt ? 0xFFFFFFFFu : cnt + dp[w];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // inclusive prefix over the bins
+        const uint32_t x = (uint32_t)__shfl((int)cnt, (lane - o) & 63, 64);
+        const uint32_t add = lane >= o ? x : 0u;
+        cnt = cnt + add < cnt ? 0xFFFFFFFFu : cnt + add;
+    }
+    if (p.tail_diag) plan.t_setup = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
+    uint32_t budget = kAnBudget;
+    for (int attempt = 0; attempt < 2; ++attempt, budget *= 4) {
+        const uint64_t fit = ballot(cnt <= budget);  // bins 0..L fit: a prefix of the lanes
+        if (!fit) continue;
+        const int L = 63 - (int)__builtin_clzll(fit);
+        const bool whole = L == 63 && hi >= full;
+        const double lim = whole ? full : (double)(L + 1) * delta * (1.0 - 0x1p-30);
+        const int er = an_enumerate<TMAX>(A, NU, t, an_fix_up(whole ? full : lim), rem0, comb0, nkern, ifrom, BM,
+                                          l0, whole ? l0 : lim, ap, budget * 2, lane, iters);
+        if (er) {
+            plan.fails |= 1 << er;
+            continue;
+        }
+        if (whole) {
+            plan.mode = 1;
+            return plan;
+        }
+        // earliest candidate with l <= lim: from its pattern on, l0 <= lim, and every
+        // improvement after it is among the enumerated candidates
         const uint64_t stop = an_earliest(A, lim, lane);
         if (stop == ~0ull) continue;
-        best_k = k;
-        best_stop = stop;
-        if (stop <= ifrom + 64ull) break;  // cannot end sooner
-    }
-    if (best_k == 0 || best_stop - ifrom > 64ull * kAnExactChunks) {
-        plan.why = best_k == 0 ? 3 : 4;
+        if (stop - ifrom > 64ull * kAnExactChunks) {
+            plan.why = 4;
+            return plan;
+        }
+        plan.mode = 2;
+        plan.stop = stop;
         return plan;
     }
-    if (cur_k != best_k) {  // the list holds a later attempt: enumerate best_k again
-        double lb = 0.0;
-        for (int q = 0; q < best_k; ++q) lb += rdlf(P.asv[0], NB + q);
-        if (!an_enumerate<TMAX>(A, NU, t, an_fix_up(lb * (1.0 + 0x1p-40)), rem0, comb0, nkern, ifrom, BM, l0,
-                                ordl, ap, kAnBudget, lane, iters))
-            { plan.why = 5; return plan; }
-    }
-    plan.mode = 2;
-    plan.stop = best_stop;
+    plan.why = 3;
     return plan;
 }
 
@@ -878,16 +1100,24 @@ __device__ void an_replay(SearchState<1> &S, const Prep<M, TMAX> &P, const AnWav
                           const double *as, const SearchParams &p, int lane) {
     const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63ull) & ~63ull) : ~0ull;
     const uint32_t nc = A->ncand < (uint32_t)kAnCand ? A->ncand : (uint32_t)kAnCand;
-    uint64_t key[1] = {~0ull};
-    if ((uint32_t)lane < nc && (uint64_t)A->cand[lane].i >= from)
-        key[0] = ((uint64_t)A->cand[lane].i << 6) | (uint64_t)lane;
-    wave_bitonic_sort<1>(key, lane);
-    for (int k = 0; k < 64; ++k) {
-        const uint64_t kk = rdl64(key[0], k);
+    constexpr int KW = kAnCand / 64;
+    static_assert(kAnCand % 64 == 0 && kAnCand <= 256, "candidate keys: (pattern << 8) | index");
+    uint64_t key[KW];
+#pragma unroll
+    for (int s = 0; s < KW; ++s) {
+        const uint32_t e = (uint32_t)(lane + 64 * s);
+        key[s] = ~0ull;
+        if (e < nc && (uint64_t)A->cand[e].i >= from) key[s] = ((uint64_t)A->cand[e].i << 8) | (uint64_t)e;
+    }
+    wave_bitonic_sort<KW>(key, lane);
+    for (int k = 0; k < 64 * KW; ++k) {
+        uint64_t kk = 0;
+#pragma unroll
+        for (int s = 0; s < KW; ++s) kk = (k >> 6) == s ? rdl64(key[s], k & 63) : kk;
         if (kk == ~0ull) break;
-        const uint64_t ii = kk >> 6;
+        const uint64_t ii = kk >> 8;
         if (ii >= S.bound || ii >= capc) break;
-        const AnCand c = A->cand[kk & 63ull];
+        const AnCand c = A->cand[kk & 255ull];
         Mask<1> d;
         d.w[0] = c.D;
         accept_success<M, TMAX>(S, P, d, (int)c.m, c.l, ii, as, p, lane);
@@ -909,7 +1139,8 @@ __device__ void an_replay(SearchState<1> &S, const Prep<M, TMAX> &P, const AnWav
 template <int M, int TMAX, bool TAB, bool AN>
 __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const uint16_t *lg,
                                 const uint32_t *col, const uint64_t *chien, double *as,
-                                double *ap, uint8_t *ordl, uint32_t cw, int lane, AnWave *an) {
+                                double *ap, uint8_t *ordl, uint32_t cw, int lane, AnWave *an,
+                                uint32_t item) {
     constexpr int NW = Geo<M>::NW;
     // analytic tail: exact chunks end at an_stop, then the candidates decide the rest
     bool an_tried = false, an_exact = false;
@@ -955,7 +1186,24 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     }
     constexpr int G = chunk_group<TAB>();
     uint32_t chunks = 0;
-    for (uint64_t base0 = 0;; base0 += 64 * G) {
+    uint64_t base00 = 0;
+    if constexpr (AN && G == 1) {
+        if (p.tail_rec && p.queue) {  // resume where the first pass handed this codeword off
+            const TailRec r = p.tail_rec[item];
+            S.l0 = r.l0;
+            S.bound = r.bound;
+            S.jsteps = r.jsteps;
+            S.impr = r.impr;
+            S.best.w[0] = r.best;
+            S.T = r.T;
+            S.m0 = r.m0;
+            S.firstOK = (r.flags & 1u) != 0;
+            S.accepted = (r.flags & 2u) != 0;
+            chunks = r.chunks;
+            base00 = 64ull * r.chunks;
+        }
+    }
+    for (uint64_t base0 = base00;; base0 += 64 * G) {
         // the checks of the next chunk before any decode (no group started past the end)
         if (base0 >= S.bound) { S.i_end = S.bound; break; }
         if (p.max_decodes && base0 >= p.max_decodes) { S.i_end = base0; S.truncated = true; break; }
@@ -965,12 +1213,15 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
                 an_tried = true;
                 uint32_t iters = 0;
                 if (p.tail_diag) dg_t2 = __builtin_amdgcn_s_memtime();
-                const AnPlan plan = an_plan<M, TMAX>(S, P, p, an, col, ordl, ap, base0, lane, iters);
+                const AnPlan plan = an_plan<M, TMAX>(S, P, p, an, col, ordl, as, ap, base0, lane, iters);
                 if (p.tail_diag) {
                     dg_t3 = __builtin_amdgcn_s_memtime();
                     dg_iters = iters;
+                    dg_t1 = dg_t2 - ((uint64_t)plan.t_setup << 20 | plan.t_elim);  // packed below
+                    dg_t0 = dg_t1 - ((uint64_t)plan.t_tab << 20 | plan.t_cls);
                     dg_mode = (uint32_t)plan.mode | ((uint32_t)plan.why << 8) |
-                              (uint32_t)(((plan.stop > base0 ? plan.stop - base0 : 0) >> 6) << 16);
+                              (uint32_t)(((plan.stop > base0 ? plan.stop - base0 : 0) >> 6) << 16) |
+                              ((uint32_t)plan.fails << 24);
                 }
                 if (p.tail_stats && lane == 0) {
                     atomicAdd(p.tail_stats + plan.mode, 1u);
@@ -1012,9 +1263,28 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
             }
             if (hand_off) {
                 if (lane == 0) {  // longest-first: large remaining bounds to the front queue
-                    uint32_t *slot = S.bound >= p.heavy_big
-                                         ? p.heavy_queue + atomicAdd(p.heavy_tail, 1u)
-                                         : p.heavy_queue + (p.count - 1u - atomicAdd(p.heavy_tail2, 1u));
+                    uint32_t *slot;
+                    if (S.bound >= p.heavy_big) {
+                        const uint32_t k = atomicAdd(p.heavy_tail, 1u);
+                        slot = p.heavy_queue + k;
+                        if constexpr (!AN && NW == 1) {
+                            if (p.tail_rec) {  // the analytic tail kernel resumes from here
+                                TailRec r;
+                                r.l0 = S.l0;
+                                r.bound = S.bound;
+                                r.jsteps = S.jsteps;
+                                r.impr = S.impr;
+                                r.best = S.best.w[0];
+                                r.T = S.T;
+                                r.m0 = S.m0;
+                                r.chunks = chunks;
+                                r.flags = (S.firstOK ? 1u : 0u) | (S.accepted ? 2u : 0u);
+                                p.tail_rec[k] = r;
+                            }
+                        }
+                    } else {
+                        slot = p.heavy_queue + (p.count - 1u - atomicAdd(p.heavy_tail2, 1u));
+                    }
                     __hip_atomic_store(slot, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 handed = true;  // redone from scratch by kaneko_coop_kernel
@@ -1077,6 +1347,40 @@ __device__ __forceinline__ void wave_done(const SearchParams &p, int lane, uint3
     }
 }
 
+// The analytic tail kernel running concurrently with the first pass: the next codeword the
+// first pass hands off (one ticket per codeword; the first pass reserves a slot with its
+// tail, then stores the codeword; consumers restore empty slots), kEmptySlot once the
+// first pass has finished (its per-XCD done counts reach *in_total) and no ticket is left.
+// Every wait is bounded (a logic error ends the wave instead of hanging it).
+__device__ uint32_t tail_dequeue(const SearchParams &p) {
+    constexpr uint32_t kTailSpin = 1u << 24;  // ~1 s of polling: a guard against logic errors
+    const uint32_t total = p.in_total ? *p.in_total : p.count;
+    const uint32_t k = atomicAdd(p.in_head, 1u);
+    for (uint32_t spins = 0; spins < kTailSpin; ++spins) {
+        if (k < ld_rlx(p.in_tail)) {
+            uint32_t *slot = p.in_queue + k;
+            for (uint32_t w = 0; w < kTailSpin; ++w) {
+                const uint32_t cw = ld_rlx(slot);
+                if (cw != kEmptySlot) {
+                    __hip_atomic_store(slot, kEmptySlot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return cw;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            return kEmptySlot;
+        }
+        uint32_t done = 0;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) done += ld_rlx(p.in_done + 32 * x);
+        const bool final = done >= total;
+        mem_drain();
+        if (k < ld_rlx(p.in_tail)) continue;
+        if (final) return kEmptySlot;
+        __builtin_amdgcn_s_sleep(16);
+    }
+    return kEmptySlot;
+}
+
 template <int M, int TMAX, bool TAB, bool AN>
 __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock)
 kaneko_search_kernel(SearchParams p) {
@@ -1096,11 +1400,26 @@ kaneko_search_kernel(SearchParams p) {
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
     AnWave *an = (AN && an_capable<M, TMAX>()) ? reinterpret_cast<AnWave *>(wbase + WB) : nullptr;
+    if constexpr (AN) {
+        if (p.in_queue) {  // concurrent with the first pass: take hand-offs as they come
+            uint32_t ndone = 0;
+            for (;;) {
+                uint32_t cw = 0;
+                if (lane == 0) cw = tail_dequeue(p);
+                cw = (uint32_t)__shfl((int)cw, 0, 64);
+                if (cw == kEmptySlot) break;
+                search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, 0u);
+                ++ndone;
+            }
+            wave_done(p, lane, ndone);
+            return;
+        }
+    }
     if (!p.queue) {
         const uint32_t stride = gridDim.x * kWavesPerBlock;
         uint32_t ndone = 0;
         for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride, ++ndone)
-            search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an);
+            search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, cw);
         wave_done(p, lane, ndone);
         return;
     }
@@ -1120,7 +1439,7 @@ kaneko_search_kernel(SearchParams p) {
             ++exhausted;
             continue;
         }
-        search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane, an);
+        search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane, an, item);
         ++ndone;
     }
     wave_done(p, lane, ndone);
