@@ -371,7 +371,7 @@ struct bchk_ctx {
     bool use_fast = true;
     size_t lds_fast = 0, lds_coop = 0;
     int grid_coop = 0, grid_coop_tab = 0;
-    uint32_t chunk_limit = 2;
+    uint32_t chunk_limit = 4;  // exact steps before a hand-off (measured best at 4-6 dB)
     DevBuf queue, heavy, ctrl, diag;  // work queues + control words (one 128-B line each)
     uint8_t *d_tables = nullptr;
     hipStream_t stream = nullptr;
@@ -390,6 +390,9 @@ struct bchk_ctx {
     bool tail_diag_on = false;     // BCHK_TAIL_DIAG=1: per-codeword tail timing records
     bool tail_concurrent = false;  // BCHK_TAIL_CONCURRENT=1: the tail kernel beside the first pass
     int tail_conc_blocks = 256;    // blocks of the concurrent tail kernel (one per CU)
+    // hybrid tail: a first-pass hand-off whose loop bound is below this goes to a cooperative
+    // kernel running beside the tail kernel instead (0: every hand-off to the tail kernel)
+    uint64_t tail_min_bound = 0;
     DevBuf tdiag;
     bool profile = false;
     // syndrome decoding table (bchk_syndtab.h): built on first use, shared across contexts
@@ -414,11 +417,13 @@ int sigma_s2(int k, int n, double snr_db, double *sd) {
 // tail / head (lines 9, 10), back tail / head (11, 12), 8 per-XCD counts of codewords the
 // exact kernel has finished (13-20), diagnostic record count (21), the first pass's
 // hand-offs to the analytic tail kernel (22), its 8 per-XCD heads (23-30) and finished
-// counts (31-38), its outcome counters (39); zeroed by one memset per decode call
-constexpr size_t kCtrlBytes = 40 * 128;
+// counts (31-38), its outcome counters (39), an always-empty queue tail and head (40, 41),
+// the hybrid tail's back-queue tail and head (42, 43); zeroed by one memset per decode call
+constexpr size_t kCtrlBytes = 44 * 128;
 constexpr int kHeavyTail = 32 * 9, kHeavyHead = 32 * 10, kHeavyTail2 = 32 * 11,
               kHeavyHead2 = 32 * 12, kExactDone = 32 * 13, kL1Tail = 32 * 22, kTailHeads = 32 * 23,
-              kTailDone = 32 * 31, kTailStats = 32 * 39;
+              kTailDone = 32 * 31, kTailStats = 32 * 39, kNoneTail = 32 * 40, kNoneHead = 32 * 41,
+              kL1Back = 32 * 42, kL1BackHead = 32 * 43;
 #ifdef BCHK_DIAG
 constexpr int kDiagCount = 32 * 21;
 #endif
@@ -519,6 +524,9 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     }
     // the tail kernel runs on the auxiliary stream, concurrently with the first pass
     const bool tconc = tail && c->tail_concurrent;
+    // hybrid: the short hand-offs to a cooperative kernel on s while the tail kernel (aux)
+    // takes the long ones; the tail's own hand-offs to a second cooperative kernel on aux
+    const bool hybrid = tail && !tconc && c->tail_min_bound > 0;
     const bool conc = c->coop_concurrent && p.heavy_tail && !tail;
     hipStream_t cs = conc ? c->aux : s;  // the cooperative kernel's stream
     bchk_ctx::Ev ev{};
@@ -547,7 +555,8 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         if (tail) {  // hand-offs (all to the front) into the tail kernel's queue
             q.heavy_queue = (uint32_t *)c->l1q.p;
             q.heavy_tail = ctrl + kL1Tail;
-            q.heavy_big = 0;
+            q.heavy_tail2 = ctrl + kL1Back;  // hybrid: loop bounds below heavy_big
+            q.heavy_big = hybrid ? c->tail_min_bound : 0;
             q.tail_rec = tconc ? nullptr : (TailRec *)c->l1rec.p;
         }
         if (fast) {
@@ -563,7 +572,11 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[3], s));
     SearchParams pc = p;  // the cooperative kernel's view of its producer
-    hipStream_t ts = tconc ? c->aux : s;  // the tail kernel's stream
+    hipStream_t ts = (tconc || hybrid) ? c->aux : s;  // the tail kernel's stream
+    if (hybrid) {
+        HIP_TRY(hipEventRecord(c->ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[6], ts));
     if (tail) {
         SearchParams q = p;
@@ -590,12 +603,29 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
             q.tail_diag_cap = (uint32_t)(c->tdiag.cap / 64);
         }
         int tgrid = tabk ? c->grid_tail_tab : c->grid_tail;
-        if (tconc) tgrid = std::min(tgrid, c->tail_conc_blocks);  // leave the first pass its CUs
+        if (tconc || hybrid) tgrid = std::min(tgrid, c->tail_conc_blocks);  // CUs for the others
         HIP_TRY(launch_tail(c->ks, q, tgrid, c->lds_tail, ts));
         pc.exact_done = ctrl + kTailDone;
         pc.exact_total = ctrl + kL1Tail;
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[7], ts));
+    if (hybrid) {
+        SearchParams ph = p;  // the first pass's short hand-offs: the back of l1q
+        ph.heavy_queue = (uint32_t *)c->l1q.p;
+        ph.heavy_tail = ctrl + kNoneTail;
+        ph.heavy_head = ctrl + kNoneHead;
+        ph.heavy_tail2 = ctrl + kL1Back;
+        ph.heavy_head2 = ctrl + kL1BackHead;
+        if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], s));
+        HIP_TRY(launch_coop(c->ks, ph, grid_coop, c->lds_coop, s));
+        if (c->profile) HIP_TRY(hipEventRecord(ev.e[5], s));
+        // the tail kernel's hand-offs (rare) after it on aux, then s waits for aux
+        HIP_TRY(launch_coop(c->ks, pc, grid_coop, c->lds_coop, c->aux));
+        HIP_TRY(hipEventRecord(c->ev_join, c->aux));
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+        if (c->profile) c->events.push_back(ev);
+        return 0;
+    }
     if (tconc) {  // the cooperative kernel (stream s) follows both
         HIP_TRY(hipEventRecord(c->ev_join, c->aux));
         HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
@@ -685,6 +715,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (getenv("BCHK_TAIL_DIAG")) c->tail_diag_on = true;
     if (const char *tc = getenv("BCHK_TAIL_CONCURRENT")) c->tail_concurrent = atoi(tc) != 0;
     if (const char *tb = getenv("BCHK_TAIL_BLOCKS")) c->tail_conc_blocks = std::max(1, atoi(tb));
+    if (const char *tm = getenv("BCHK_TAIL_MIN_BOUND")) c->tail_min_bound = strtoull(tm, nullptr, 10);
     c->lds_coop = tb + c->ks.coop_bytes;
     // one cooperative workgroup per CU by default (LDS sized past half the CU's 160 KB):
     // a heavy codeword's 16 waves then own the CU's four SIMDs, which shortens the longest

@@ -598,7 +598,7 @@ struct AnPend {  // a codeword met by the enumeration, emitted in batches of 64
     uint32_t sel, comb;
     int64_t usum;
 };
-constexpr int kAnPend = 128;
+constexpr int kAnPend = 64 + 5 * 64;  // below 64 between steps, + 5 pushes of a wave
 struct AnWave {
     AnNode stack[kAnStack];
     AnCand cand[kAnCand];
@@ -742,70 +742,81 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         const int depth = __popc(nd.sel);
         const int next = (int)nd.next;
         const int q = next < NU ? next : NU;  // NU: the sentinel (never fits)
+        const int qr = next < NU ? next : 0;
+        // every load of the step at once: the child's reliability and the next one's, its
+        // residual and pattern bits, the class mask of this node's residual
+        const int64_t aq = A->afix[q];
+        const int64_t anext = A->afix[q + 1 <= NU ? q + 1 : NU];
+        const uint64_t rq = A->ru[qr];
+        const uint32_t cq = A->cu[qr];
+        uint32_t cl = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (i < cbits) cl |= (uint32_t)((nd.rem >> cpiv[i]) & 1ull) << i;
+        const uint32_t cmk = A->cmask[cbits >= 0 ? cl : 0];
         const int64_t X = limfix - nd.sum;
-        const bool valid = have && next < NU && depth < t && A->afix[q] <= X;
-        const int qc = valid ? q : 0;
-        const int64_t aq = A->afix[qc];
-        const int64_t anext = A->afix[qc + 1 <= NU ? qc + 1 : NU];
+        const bool valid = have && next < NU && depth < t && aq <= X;
         const int64_t cs = nd.sum + aq;
-        const bool expand = valid && depth + 1 < t && qc + 1 < NU && anext <= limfix - cs;
+        const bool expand = valid && depth + 1 < t && q + 1 < NU && anext <= limfix - cs;
         // no child from q on can expand (the pair sums ascend): all of them are leaves, and
         // the ones whose residual matches are found from the class masks at once
         const bool run = valid && !expand && cbits >= 0;
         const bool single = valid && !run;
         // a single child (visited one per step)
-        const uint64_t crem = nd.rem ^ A->ru[qc];
-        const uint32_t ccomb = nd.comb ^ A->cu[qc];
-        const uint32_t csel = nd.sel | (1u << qc);
-        // a leaf run from q on: of the remaining children only those whose residual
-        // matches can be codewords; walked in ascending order until one is over the bound
-        uint32_t matches = 0;
-        if (run) {
-            uint32_t cl = 0;
-#pragma unroll
-            for (int i = 0; i < 5; ++i)
-                if (i < cbits) cl |= (uint32_t)((nd.rem >> cpiv[i]) & 1ull) << i;
-            matches = A->cmask[cl] & ~((1u << qc) - 1u);
-        }
-        (void)nodes;
+        const uint64_t crem = nd.rem ^ rq;
+        const uint32_t ccomb = nd.comb ^ cq;
+        const uint32_t csel = nd.sel | (1u << qr);
         // codewords (zero residual) that can still reach a pattern below BM wait for the
         // next batch of emissions (a whole wave processes 64 together)
-        bool pend = single && crem == 0ull && (nkern > 0 || __popc(ccomb >> jb) <= t - depth - 1);
-        uint32_t psel = csel, pcomb = ccomb;
-        int64_t psum = cs;
-        for (;;) {
-            const uint64_t pm = ballot(pend);
-            if (pm == 0ull && ballot(matches != 0u) == 0ull) break;
-            if (pend) {
+        auto push = [&](bool c, uint32_t sel, uint32_t comb, int64_t sum) {
+            const uint64_t pm = ballot(c);
+            if (c) {
                 AnPend e;
-                e.sel = psel;
-                e.comb = pcomb;
-                e.usum = psum;
+                e.sel = sel;
+                e.comb = comb;
+                e.usum = sum;
                 A->pend[np + __popcll(pm & below)] = e;
             }
             np += __popcll(pm);
-            if (np >= 64) {
+        };
+        auto drain = [&]() {
+            while (np >= 64) {
                 wave_sync();
                 const AnPend e = A->pend[np - 1 - lane];
                 an_emit<TMAX>(A, e.sel, e.usum, e.comb, __popc(e.sel), t, nkern, ifrom, BM, jb, l0, lcap, ap);
                 np -= 64;
                 wave_sync();
             }
-            // next match of this lane's leaf run (the run ends at the first one over the bound)
-            pend = false;
-            if (matches) {
-                const int m = __builtin_ctz(matches);
-                matches &= matches - 1u;
-                const int64_t am = A->afix[m];
-                if (am <= X) {
-                    psel = nd.sel | (1u << m);
-                    pcomb = nd.comb ^ A->cu[m];
-                    psum = nd.sum + am;
-                    pend = nkern > 0 || __popc(pcomb >> jb) <= t - depth - 1;
-                } else {
-                    matches = 0;
-                }
+        };
+        push(single && crem == 0ull && (nkern > 0 || __popc(ccomb >> jb) <= t - depth - 1), csel, ccomb, cs);
+        drain();
+        // a leaf run from q on: of the remaining children only those whose residual
+        // matches can be codewords, ascending until one is over the bound; 4 at a time
+        uint32_t mm = run ? (cmk & ~((1u << qr) - 1u)) : 0u;
+        while (ballot(mm != 0u)) {
+            int mi[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                mi[i] = mm ? (int)__builtin_ctz(mm) : NU;
+                mm &= mm - 1u;
             }
+            int64_t av[4];
+            uint32_t cv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                av[i] = A->afix[mi[i]];
+                cv[i] = A->cu[mi[i] < NU ? mi[i] : 0];
+            }
+            bool stop = false;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                stop = stop || !(av[i] <= X);  // the sentinel at NU never fits
+                const uint32_t pc = nd.comb ^ cv[i];
+                push(!stop && (nkern > 0 || __popc(pc >> jb) <= t - depth - 1), nd.sel | (1u << (mi[i] & 31)), pc,
+                     nd.sum + av[i]);
+            }
+            if (stop) mm = 0u;
+            drain();
         }
         // the parent stays open iff its next child fits too
         const bool cont = expand && anext <= X;
@@ -814,7 +825,7 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         if (sp + cnt > kAnStack) return 2;
         if (cont) {
             AnNode c = nd;
-            c.next = (uint32_t)(qc + 1);
+            c.next = (uint32_t)(q + 1);
             A->stack[sp + __popcll(em & below)] = c;
         }
         sp += cnt;
@@ -824,7 +835,7 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
             nd.sel = csel;
             nd.comb = ccomb;
         }
-        nd.next = (uint32_t)(qc + 1);
+        nd.next = (uint32_t)(q + 1);
         const bool valid_next = single;  // a leaf run ends the node
         have = valid_next;
         wave_sync();
@@ -1008,10 +1019,10 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     if (p.tail_diag) plan.t_tab = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
     const double l0 = S.l0;
     const double full = l0 * (1.0 + 0x1p-40);
-    // No U subset of 3 or more fits under l0: at most 1 + NU + NU (NU - 1) / 2 nodes, so the
+    // No U subset of 4 or more fits under l0: at most 1 + 32 + 496 + 4960 nodes, so the
     // complete enumeration goes ahead without counting.
-    if (NU < 3 || t <= 2 ||
-        rdlf(P.asv[0], NB) + rdlf(P.asv[0], NB + 1) + rdlf(P.asv[0], NB + 2) > full) {
+    if (NU < 4 || t <= 3 ||
+        rdlf(P.asv[0], NB) + rdlf(P.asv[0], NB + 1) + rdlf(P.asv[0], NB + 2) + rdlf(P.asv[0], NB + 3) > full) {
         if (p.tail_diag) plan.t_setup = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
         const int er = an_enumerate<TMAX>(A, NU, t, an_fix_up(full), rem0, comb0, nkern, ifrom, BM, l0, l0, ap,
                                           2 * kAnBudget, lane, iters);
@@ -1042,11 +1053,15 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     for (int q = 0; q < NU; ++q) {
         const int b = (int)rdl((uint32_t)mybin, NB + q);
         if (b >= 64) break;  // ascending: no later element fits a bin either
+        // every weight's shifted counts first (the permutes issue back to back), then the adds
+        uint32_t from[TMAX];
+        const int src = ((lane - b) & 63) << 2;
 #pragma unroll
-        for (int w = TMAX; w >= 1; --w) {
-            if (w > t) continue;
-            const uint32_t from = (uint32_t)__shfl((int)dp[w - 1], (lane - b) & 63, 64);
-            const uint32_t add = lane >= b ? from : 0u;
+        for (int w = 1; w <= TMAX; ++w)
+            from[w - 1] = w <= t ? (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)dp[w - 1]) : 0u;
+#pragma unroll
+        for (int w = 1; w <= TMAX; ++w) {
+            const uint32_t add = lane >= b ? from[w - 1] : 0u;
             dp[w] = dp[w] + add < dp[w] ? 0xFFFFFFFFu : dp[w] + add;  // saturating
         }
     }
@@ -1147,7 +1162,7 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     uint64_t an_stop = 0;
     (void)an_tried;
     // analytic-tail timing records (p.tail_diag, diagnostics only): cycles per phase
-    uint64_t dg_t0 = 0, dg_t1 = 0, dg_t2 = 0, dg_t3 = 0;
+    uint64_t dg_t0 = 0, dg_t1 = 0, dg_t2 = 0, dg_t3 = 0, dg_stage = 0;
     uint32_t dg_iters = 0, dg_mode = 0;
     if (AN && p.tail_diag) dg_t0 = __builtin_amdgcn_s_memtime();
     Prep<M, TMAX> P;
@@ -1162,13 +1177,13 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
             if (r < p.tail_diag_cap) {
                 unsigned long long *d = p.tail_diag + (size_t)r * 8;
                 const uint64_t t4 = __builtin_amdgcn_s_memtime();
-                d[0] = cw;
-                d[1] = dg_t1 - dg_t0;
-                d[2] = dg_t2 - dg_t1;
-                d[3] = dg_t3 - dg_t2;
-                d[4] = dg_iters;
+                d[0] = cw | (uint64_t)xcc_id() << 24 | (dg_t0 & 0xFFFFFFFFFull) << 28;  // + XCD, start
+                d[1] = dg_t1 - dg_t0;                         // prep (+ resume)
+                d[2] = dg_stage;                              // plan stages (packed)
+                d[3] = dg_t3 - dg_t2;                         // plan
+                d[4] = dg_iters | (uint64_t)(dg_t2 - dg_t1) << 32;  // steps, exact chunks before
                 d[5] = dg_mode;
-                d[6] = t4 - dg_t3;
+                d[6] = t4 - dg_t3;                            // split chunks + replay + outputs
                 d[7] = S.i_end;
             }
         }
@@ -1217,8 +1232,9 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
                 if (p.tail_diag) {
                     dg_t3 = __builtin_amdgcn_s_memtime();
                     dg_iters = iters;
-                    dg_t1 = dg_t2 - ((uint64_t)plan.t_setup << 20 | plan.t_elim);  // packed below
-                    dg_t0 = dg_t1 - ((uint64_t)plan.t_tab << 20 | plan.t_cls);
+                    const auto c16 = [](uint32_t x) { return (uint64_t)(x < 0xFFFFu ? x : 0xFFFFu); };
+                    dg_stage = c16(plan.t_elim) | c16(plan.t_cls) << 16 | c16(plan.t_tab) << 32 |
+                               c16(plan.t_setup) << 48;  // cycles from the plan's start
                     dg_mode = (uint32_t)plan.mode | ((uint32_t)plan.why << 8) |
                               (uint32_t)(((plan.stop > base0 ? plan.stop - base0 : 0) >> 6) << 16) |
                               ((uint32_t)plan.fails << 24);

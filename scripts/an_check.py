@@ -34,7 +34,9 @@ for (m, t, J, snr, B) in [(6, 6, 15, 5.0, 1 << 16), (6, 6, 15, 4.0, 1 << 16), (6
                           (6, 6, -1, 5.0, 1 << 15), (6, 6, -1, 4.0, 1 << 12), (6, 6, 15, 6.0, 1 << 16),
                           (5, 3, 15, 2.0, 1 << 15), (5, 3, -1, 3.0, 1 << 14), (6, 4, 15, 4.0, 1 << 14),
                           (5, 5, 15, 3.0, 1 << 14), (4, 2, 15, 1.0, 1 << 14)]:
-    os.environ["BCHK_TAIL_CONCURRENT"] = str(int(snr) % 2)  # both tail launch modes
+    mode = int(snr * 2 + m) % 3  # the tail launch modes: sequential, concurrent, hybrid
+    os.environ["BCHK_TAIL_CONCURRENT"] = str(int(mode == 1))
+    os.environ["BCHK_TAIL_MIN_BOUND"] = "1023" if mode == 2 else "0"
     on, off = mk(m, t, J, True), mk(m, t, J, False)
     _, y, _ = on.generate(snr, B, seed=12345)
     if J < 0:
@@ -67,9 +69,10 @@ for (m, t, J, snr, B) in [(6, 6, 15, 5.0, 1 << 16), (6, 6, 15, 4.0, 1 << 16), (6
 
 # timing of the headline batch per stage
 for J, snr in [(15, 5.0), (15, 4.0), (15, 6.0), (-1, 5.0)]:
-    for analytic, limit, conc in [(False, 4, 0), (True, 2, 0), (True, 4, 0), (True, 1, 1), (True, 2, 1),
-                                  (True, 4, 1)]:
+    for analytic, limit, conc, hyb in [(False, 4, 0, 0), (True, 2, 0, 0), (True, 3, 0, 0), (True, 4, 0, 0),
+                                       (True, 4, 1, 0), (True, 4, 0, 1023)]:
         os.environ["BCHK_TAIL_CONCURRENT"] = str(conc)
+        os.environ["BCHK_TAIL_MIN_BOUND"] = str(hyb)
         d = mk(6, 6, J, analytic, limit)
         _, y, _ = d.generate(snr, 1 << 20, seed=1)
         import torch
@@ -92,7 +95,7 @@ for J, snr in [(15, 5.0), (15, 4.0), (15, 6.0), (-1, 5.0)]:
         st, n = d.profile_read_stages()
         d.profile(False)
         ex, co = d.path_counts()
-        print(json.dumps({"J": J, "snr": snr, "analytic": analytic, "chunk_limit": limit, "conc": conc,
+        print(json.dumps({"J": J, "snr": snr, "analytic": analytic, "chunk_limit": limit, "conc": conc, "hybrid": hyb,
                           "ms_per_call": round(ms, 4),
                           "stage_ms": [round(x / n, 4) for x in st], "to_exact": ex, "to_tail": d.tail_count(), "tail_stats": d.tail_stats(),
                           "to_coop": co}), flush=True)
