@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="reference processes for the CPU baseline (0 = the host's core share)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--unfused", action="store_true",
+                    help="decode_device + count_device (re-reads res and stats) instead of the fused call")
     return ap.parse_args()
 
 
@@ -193,10 +195,14 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
     def step():
         # everything below is enqueued on the decoder's stream (torch ops via ExternalStream)
         d_step.zero_()
-        dec.decode_device(d_y.data_ptr(), B, d_res.data_ptr(), d_l0.data_ptr(), d_st.data_ptr(),
-                          dec.stream)
-        dec.count_device(d_tx.data_ptr(), d_res.data_ptr(), d_st.data_ptr(), B, d_step.data_ptr(),
-                         dec.stream)
+        if args.unfused:  # decode, then the counters from a re-read of res / stats
+            dec.decode_device(d_y.data_ptr(), B, d_res.data_ptr(), d_l0.data_ptr(), d_st.data_ptr(),
+                              dec.stream)
+            dec.count_device(d_tx.data_ptr(), d_res.data_ptr(), d_st.data_ptr(), B, d_step.data_ptr(),
+                             dec.stream)
+        else:  # counters fused into the decode kernels (no per-codeword stats stored)
+            dec.decode_count_device(d_y.data_ptr(), d_tx.data_ptr(), B, d_res.data_ptr(), d_l0.data_ptr(), 0,
+                                    d_step.data_ptr(), dec.stream)
         reduce_step(d_step, d_cnt, world, dist)
 
     with torch.cuda.stream(stream):

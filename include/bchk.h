@@ -108,6 +108,15 @@ int bchk_alg_decode_host(bchk_ctx *ctx, const uint8_t *words, const uint32_t *sy
  * tx/res [B][n]; st [B] from bchk_decode_device. d_out6 is a device uint64_t[6]. */
 int bchk_count_device(bchk_ctx *ctx, const uint8_t *d_tx, const uint8_t *d_res,
                       const bchk_stats *d_st, size_t B, uint64_t *d_out6, void *stream);
+/* bchk_decode_device and bchk_count_device in one pass (the body of the reference's fun()
+ * loop over a batch, src/dataForPlot.cpp:55-74): every kernel that finishes a codeword
+ * compares its row with tx and adds to the counters, so res and st are not read back.
+ *   d_st may be NULL (then no per-codeword stats are stored; the counters still include
+ *   decodes, comparisons and sums); out6 += {frame errors, bit errors, decodes,
+ *   comparisons, sums, words}. Rows never accepted keep the caller's contents and are
+ *   counted as such, exactly as bchk_count_device after bchk_decode_device. */
+int bchk_decode_count_device(bchk_ctx *ctx, const double *d_y, const uint8_t *d_tx, size_t B, uint8_t *d_res,
+                             double *d_l0, bchk_stats *d_st, uint64_t *d_out6, void *stream);
 
 /* The reference's input stream (src/bchCoder.cpp:228-250 in fun() order): minstd_rand0
  * seeded with `seed`, B words at Eb/N0 snr_db: tx [B][n], y [B][n]. rng_state (in/out,
@@ -137,6 +146,22 @@ int bchk_sweep_block(bchk_ctx *ctx, double snr_db, uint64_t *rng_state, size_t s
  * reference's global engine would be. batch = codewords per GPU launch (0 = auto). */
 int bchk_sweep(bchk_ctx *ctx, long p, long e, double max_snr, uint64_t *rng_state,
                uint64_t seed, size_t batch, char *csv, size_t cap);
+
+/* On-GPU channel front-end (the encode + AWGN step of src/bchCoder.cpp:120-132,243-250 as a
+ * batched kernel): words [word0, word0 + B) of a counter-based stream (Philox4x32-10 keyed
+ * by seed; word w depends only on (seed, w)) at Eb/N0 snr_db -- uniform information bits,
+ * c(x) = info(x) g(x), y = BPSK(c) + N(0, sd) with sd as src/dataForPlot.cpp:45. The same
+ * distribution as the reference's words, NOT its minstd_rand0 stream (bchk_generate_host is
+ * the bit-exact one). d_tx [B][n] u8, d_y [B][n] f64 on device. */
+int bchk_generate_device(bchk_ctx *ctx, double snr_db, size_t B, uint64_t seed, uint64_t word0,
+                         uint8_t *d_tx, double *d_y, void *stream);
+/* fun() (src/dataForPlot.cpp:16-74) end to end on the GPU: words from bchk_generate_device,
+ * decode and counters fused (bchk_decode_count_device), Eb/N0 0..max_snr step 0.5, each point
+ * until p words or e frame errors (the e-th error cut exactly in word order). CSV lines as
+ * bchk_sweep (statistically the reference's, not byte-identical); seconds = wall time,
+ * words = words decoded. */
+int bchk_sweep_device(bchk_ctx *ctx, long p, long e, double max_snr, uint64_t seed, size_t batch,
+                      char *csv, size_t cap, double *seconds, uint64_t *words);
 
 int bchk_sync(bchk_ctx *ctx);
 /* the context's HIP stream (hipStream_t) */

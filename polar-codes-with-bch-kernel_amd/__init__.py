@@ -30,8 +30,8 @@ F_ACCEPTED, F_RETURNED, F_TRUNCATED, F_TIE, F_SCAN_UB = 1, 2, 4, 8, 16
 EXPORTS = (
     "bchk_create", "bchk_destroy", "bchk_code_params", "bchk_generator",
     "bchk_set_max_decodes", "bchk_decode_host", "bchk_decode_device",
-    "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device",
-    "bchk_generate_host", "bchk_generate_host_draws", "bchk_rng_jump", "bchk_sweep_block", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
+    "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device", "bchk_decode_count_device",
+    "bchk_generate_host", "bchk_generate_host_draws", "bchk_generate_device", "bchk_sweep_device", "bchk_rng_jump", "bchk_sweep_block", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
     "bchk_profile_read", "bchk_profile_read_stages", "bchk_path_counts", "bchk_tail_count",
     "bchk_tail_stats", "bchk_tail_diag_read", "bchk_set_fast_path", "bchk_set_analytic",
     "bchk_set_chunk_limit", "bchk_set_syndrome_table",
@@ -86,6 +86,10 @@ def lib():
     L.bchk_decode_variant_host.argtypes = [vp, i32, vp, sz, vp, vp, vp]
     L.bchk_alg_decode_host.argtypes = [vp, vp, vp, sz, vp, vp]
     L.bchk_count_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
+    L.bchk_decode_count_device.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    L.bchk_generate_device.argtypes = [vp, C.c_double, sz, u64, u64, vp, vp, vp]
+    L.bchk_sweep_device.argtypes = [vp, C.c_long, C.c_long, C.c_double, u64, sz, C.c_char_p, sz,
+                                    C.POINTER(C.c_double), C.POINTER(u64)]
     L.bchk_generate_host.argtypes = [vp, dbl, sz, C.POINTER(u64), u64, vp, vp]
     L.bchk_generate_host_draws.argtypes = [vp, dbl, sz, C.POINTER(u64), u64, vp, vp, C.POINTER(u64)]
     L.bchk_rng_jump.argtypes = [u64, u64]
@@ -192,6 +196,12 @@ class KanekoKernelProcessor:
                                        C.c_void_p(d_st), B, C.c_void_p(d_out6),
                                        C.c_void_p(stream) if stream else None))
 
+    def decode_count_device(self, d_y, d_tx, B, d_res, d_l0, d_st, d_out6, stream=None):
+        """decode_device + count_device fused (bchk_decode_count_device); d_st may be 0."""
+        _check(lib().bchk_decode_count_device(self._h, C.c_void_p(d_y), C.c_void_p(d_tx), B, C.c_void_p(d_res),
+                                              C.c_void_p(d_l0), C.c_void_p(d_st) if d_st else None,
+                                              C.c_void_p(d_out6), C.c_void_p(stream) if stream else None))
+
     def alg_decode(self, words, syndromes=None):
         """Decoder::decode batch: words [N, n] u8 -> (ok [N] bool, answers [N, n] u8)."""
         words = np.ascontiguousarray(np.atleast_2d(words), np.uint8)
@@ -241,6 +251,19 @@ class KanekoKernelProcessor:
         st = C.c_uint64(state)
         _check(lib().bchk_sweep(self._h, p, e, max_snr, C.byref(st), seed, batch, buf, len(buf)))
         return (buf.value.decode(), st.value) if return_state else buf.value.decode()
+
+    def generate_device(self, snr, B, d_tx, d_y, seed=1, word0=0, stream=None):
+        """On-GPU channel: words [word0, word0 + B) of the counter-based stream into d_tx, d_y."""
+        _check(lib().bchk_generate_device(self._h, snr, B, seed, word0, C.c_void_p(d_tx), C.c_void_p(d_y),
+                                          C.c_void_p(stream) if stream else None))
+
+    def sweep_device(self, p, e, max_snr=5.0, seed=1, batch=0):
+        """fun() with GPU-generated words: (CSV text, seconds, words decoded)."""
+        buf = C.create_string_buffer(1 << 16)
+        secs, words = C.c_double(0.0), C.c_uint64(0)
+        _check(lib().bchk_sweep_device(self._h, p, e, max_snr, seed, batch, buf, len(buf), C.byref(secs),
+                                       C.byref(words)))
+        return buf.value.decode(), secs.value, words.value
 
     def sync(self):
         _check(lib().bchk_sync(self._h))

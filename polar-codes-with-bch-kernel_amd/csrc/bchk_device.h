@@ -110,6 +110,28 @@ struct SearchParams {
     unsigned long long *tail_diag;
     uint32_t *tail_diag_count;
     uint32_t tail_diag_cap;
+    // FER/BER/op counters fused into the decode (null = off): every kernel that finishes a
+    // codeword compares its row with the sent word tx [B][n] and adds {frame errors, bit
+    // errors, decodes, comparisons, sums, words} to the partial counters
+    // cnt[kCntSlots][kCntStride] (slot by codeword, spreading the atomics), which
+    // cnt_reduce_kernel folds into the caller's totals
+    const uint8_t *tx;
+    unsigned long long *cnt;
+};
+constexpr int kCntSlots = 512;
+constexpr int kCntStride = 16;  // u64 per slot: one 128-B line
+
+// on-GPU channel (bchk_channel.hip): words [word0, word0 + count) of the counter-based
+// stream `seed`: tx [count][n] (0/1), y [count][n] = BPSK(tx) + N(0, sd)
+struct ChanParams {
+    uint8_t *tx;
+    double *y;
+    uint64_t word0;
+    uint32_t count;
+    int32_t n, k;
+    uint32_t seed_lo, seed_hi;
+    double sd;
+    uint64_t g[4];  // generator polynomial, bit j = coefficient of x^j
 };
 
 struct AlgParams {

@@ -28,6 +28,7 @@ namespace {
 constexpr int kRowD = 9;  // doubles per staged row slice (8 + 1 pad: conflict-free b64)
 constexpr int kSlice = 8;
 constexpr int kFastWaves = 8;  // waves per persistent block
+constexpr int kStageBytes = 64 * kRowD * 8;
 }  // namespace
 
 // 32-bit sort key: a monotone 26-bit prefix of |y| (5 exponent bits covering
@@ -62,8 +63,7 @@ kaneko_fast_kernel(SearchParams p) {
     const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
     const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double *stage = reinterpret_cast<double *>(smem + ((p.td.bytes + 15) & ~15u) +
-                                               wid * (64 * kRowD * 8));
+    double *stage = reinterpret_cast<double *>(smem + ((p.td.bytes + 15) & ~15u) + wid * kStageBytes);
     const uint32_t cw0 = (blockIdx.x * kFastWaves + wid) * 64u;
     if (cw0 >= p.count) return;
     const uint32_t cw = cw0 + (uint32_t)lane;
@@ -72,6 +72,7 @@ kaneko_fast_kernel(SearchParams p) {
     (void)M;
     const double s2 = p.s2;
     const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
+    static_assert(64 * N + 256 <= kStageBytes, "output block and row errors fit the stage");
 
 #ifdef BCHK_DIAG
     // stamps: [0] stage+keys, [1] sort, [2] S0, [3] decode i=0 + accept, [4] i=1, [5] outputs
@@ -280,8 +281,20 @@ kaneko_fast_kernel(SearchParams p) {
     if (p.l0 && live) p.l0[cw] = (double)(l0 + (double)(state ^ (uint32_t)best));
     return;
 #endif
-    // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371)
-    const bool need1 = live && !bad && !ok0;
+    // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371). When the
+    // hard decision is a codeword (zero syndrome, which the decoder rejects), pattern 1 flips
+    // the least reliable position o0 and its syndrome is o0's single column: the decoder
+    // corrects that one error, back to yH, so D = 0 (l = 0) without a decode.
+    bool zero0 = true;
+#pragma unroll
+    for (int w = 0; w < W; ++w) zero0 = zero0 && S0[w] == 0u;
+    if (live && !bad && !ok0 && zero0) {
+        double l;
+        bool ret;
+        accept(0ull, l, ret);
+        if (ret) { state = 2; best = 0ull; l0 = l; }
+    }
+    const bool need1 = live && !bad && !ok0 && !zero0;
     if (ballot(need1)) {
         uint32_t S1[W];
 #pragma unroll
@@ -316,6 +329,54 @@ kaneko_fast_kernel(SearchParams p) {
     } else {
         const int rows = (int)((p.count - cw0) < 64u ? (p.count - cw0) : 64u);
         for (int i = lane; i < rows * N; i += 64) dst[i] = out[i];
+    }
+    if (p.cnt) {
+        // fused counters (src/dataForPlot.cpp:55-74) of the resolved rows: the sent words'
+        // block against the output block, 16 B at a time; differing bytes are rare
+        uint32_t *rowerr = reinterpret_cast<uint32_t *>(out + 64 * N);
+        rowerr[lane] = 0u;
+        wave_sync();
+        const uint8_t *txb = p.tx + (size_t)cw0 * N;
+        if (cw0 + 64u <= p.count && ((reinterpret_cast<uintptr_t>(txb) & 15u) == 0)) {
+            const uint4 *a4 = reinterpret_cast<const uint4 *>(txb);
+            const uint4 *b4 = reinterpret_cast<const uint4 *>(out);
+            for (int v = lane; v < 4 * N; v += 64) {
+                const uint4 a = a4[v], b = b4[v];
+                const uint32_t xx[4] = {a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (!xx[k]) continue;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if ((xx[k] >> (8 * q)) & 0xFFu) atomicAdd(&rowerr[(16 * v + 4 * k + q) / N], 1u);
+                }
+            }
+        } else {
+            const int rows = (int)((p.count - cw0) < 64u ? (p.count - cw0) : 64u);
+            for (int i = lane; i < rows * N; i += 64)
+                if (txb[i] != out[i]) atomicAdd(&rowerr[i / N], 1u);
+        }
+        wave_sync();
+        const uint32_t e = resolved ? rowerr[lane] : 0u;
+        const uint64_t it = state == 2 ? 1ull : 0ull;
+        const uint64_t pro = p.variant == BCHK_VARIANT_WORD ? (uint64_t)(2 * N + 1) : 0ull;
+        unsigned long long c[6] = {e ? 1ull : 0ull, e, resolved ? it + 1 : 0ull,
+                                   resolved ? pro + it * (uint64_t)(N + 6) : 0ull,
+                                   resolved ? pro + it * (uint64_t)(N + 1) : 0ull, resolved ? 1ull : 0ull};
+        // frame / bit errors are rare: a ballot decides whether they need a reduction
+        const bool anyerr = ballot(e != 0u) != 0ull;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            if (k < 2 && !anyerr) continue;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) c[k] += (unsigned long long)__shfl_xor((long long)c[k], o, 64);
+        }
+        if (lane == 0) {
+            unsigned long long *dst6 = p.cnt + (size_t)((cw0 >> 6) % (uint32_t)kCntSlots) * kCntStride;
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (c[k]) atomicAdd(dst6 + k, c[k]);
+        }
     }
     if (resolved) {
         const bool word = p.variant == BCHK_VARIANT_WORD;
@@ -364,7 +425,7 @@ static hipError_t launch_fast_impl(const SearchParams &p, size_t lds, hipStream_
     return hipGetLastError();
 }
 
-size_t fast_wave_bytes() { return (size_t)64 * kRowD * 8; }
+size_t fast_wave_bytes() { return (size_t)kStageBytes; }
 int fast_block_waves() { return kFastWaves; }
 
 // Fast-path instantiations (n <= 63, small t): (m, TMAX) as in select_kernels.

@@ -18,6 +18,7 @@
 #include <mutex>
 #include <random>
 #include <thread>
+#include <chrono>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -372,17 +373,28 @@ struct bchk_ctx {
     size_t lds_fast = 0, lds_coop = 0;
     int grid_coop = 0, grid_coop_tab = 0;
     uint32_t chunk_limit = 4;  // exact steps before a hand-off (measured best at 4-6 dB)
-    DevBuf queue, heavy, ctrl, diag;  // work queues + control words (one 128-B line each)
+    DevBuf diag;
+    // One decode pipeline per sub-batch: its work queues, control words (one 128-B line
+    // each) and streams. A call splits a large batch over npipes pipelines, each on its own
+    // stream, with every fast kernel after the one before it: one sub-batch's fast kernel
+    // (HBM-bound, the whole chip) runs while the sub-batches before it drain their
+    // latency-bound search / tail kernels.
+    struct Pipe {
+        DevBuf queue, heavy, ctrl, l1q, l1rec;  // l1q / l1rec: first pass -> analytic tail
+        hipStream_t s = nullptr, aux = nullptr;  // s unused for pipe 0 (the caller's stream)
+        hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_done = nullptr, ev_fast = nullptr;
+    };
+    std::vector<Pipe> pipes;
+    int npipes = 1;              // BCHK_PIPES (sub-batch pipelines; 1 = off)
+    int last_pipes = 0;          // pipelines the last call used
+    size_t pipe_min = 1u << 17;  // codewords per sub-batch at least
+    hipEvent_t ev_start = nullptr;
     uint8_t *d_tables = nullptr;
     hipStream_t stream = nullptr;
     size_t lds = 0, lds_alg = 0, lds_tail = 0;
     int grid = 0, grid_tab = 0, grid_tail = 0, grid_tail_tab = 0;
-    DevBuf l1q, l1rec;  // first pass -> analytic tail kernel: codewords, their states
     uint64_t max_decodes = 0;
     DevBuf y, res, l0, st, words, synd, ok;
-    // the cooperative kernel runs on `aux`, concurrently with the exact kernel
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool coop_concurrent = false;  // BCHK_COOP_CONCURRENT=1: measured neutral at 5 dB
     bool analytic = true;          // analytic tail of heavy codewords (BCHK_NO_ANALYTIC=1: off)
     uint64_t last_tail = 0;        // codewords the last call handed to the tail kernel
@@ -394,11 +406,16 @@ struct bchk_ctx {
     // kernel running beside the tail kernel instead (0: every hand-off to the tail kernel)
     uint64_t tail_min_bound = 0;
     DevBuf tdiag;
+    DevBuf cnt;  // fused FER/op counters: kCntSlots partial slots
+    DevBuf gtx, gy, gres, gst, gcnt, gflags;  // bchk_sweep_device's batch buffers
     bool profile = false;
     // syndrome decoding table (bchk_syndtab.h): built on first use, shared across contexts
     bool use_table = true;
     SyndTable tab{};
-    struct Ev { hipEvent_t e[8]; };  // [fast, exact, coop, tail] x [start, end] of one call
+    struct Ev {  // [fast, exact, coop, tail] x [start, end] of one pipeline of one call
+        hipEvent_t e[8];
+        bool first;  // the call's first pipeline
+    };
     std::vector<Ev> events;
     double prof_ms[4] = {0.0, 0.0, 0.0, 0.0};
     uint64_t prof_launches = 0;
@@ -431,13 +448,46 @@ constexpr int kDiagCount = 32 * 21;
 // queue (2^12 - 1: T >= 12 patterns left)
 constexpr uint64_t kHeavyBig = 4095;
 
-int ensure_heavy(bchk_ctx *c, size_t B) {
-    if (B <= c->heavy.cap / sizeof(uint32_t)) return 0;
-    int rc = c->heavy.ensure(B * sizeof(uint32_t));
+int ensure_heavy(bchk_ctx::Pipe &P, size_t B, hipStream_t s) {
+    if (B <= P.heavy.cap / sizeof(uint32_t)) return 0;
+    int rc = P.heavy.ensure(B * sizeof(uint32_t));
     if (rc) return rc;
-    // empty slots (consumers restore them after every read)
-    HIP_TRY(hipMemset(c->heavy.p, 0xFF, c->heavy.cap));
+    // empty slots (consumers restore them after every read); ordered before the pipeline's
+    // kernels on its stream (a null-stream memset is not, for non-blocking streams)
+    HIP_TRY(hipMemsetAsync(P.heavy.p, 0xFF, P.heavy.cap, s));
     return 0;
+}
+
+int ensure_pipes(bchk_ctx *c, int K) {
+    if (!c->ev_start) HIP_TRY(hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+    while ((int)c->pipes.size() < K) {
+        c->pipes.emplace_back();
+        bchk_ctx::Pipe &P = c->pipes.back();
+        if (c->pipes.size() > 1) HIP_TRY(hipStreamCreateWithFlags(&P.s, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&P.aux, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&P.ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&P.ev_done, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&P.ev_fast, hipEventDisableTiming));
+    }
+    return 0;
+}
+
+void release_pipes(bchk_ctx *c) {
+    for (auto &P : c->pipes) {
+        P.queue.release();
+        P.heavy.release();
+        P.ctrl.release();
+        P.l1q.release();
+        P.l1rec.release();
+        if (P.s) (void)hipStreamDestroy(P.s);
+        if (P.aux) (void)hipStreamDestroy(P.aux);
+        for (hipEvent_t e : {P.ev_fork, P.ev_join, P.ev_done, P.ev_fast})
+            if (e) (void)hipEventDestroy(e);
+    }
+    c->pipes.clear();
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    c->ev_start = nullptr;
 }
 
 // The context's device copy of the syndrome decoding table (first decode call; no-op when
@@ -470,16 +520,14 @@ int ensure_table(bchk_ctx *c) {
 // and -- concurrently, on the auxiliary stream -- the cooperative kernel, which takes heavy
 // codewords as soon as the exact kernel hands them off (longest first). The launch stream
 // waits for the cooperative kernel before the call's work counts as done.
-int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t *d_res,
-                  double *d_l0, bchk_stats *d_st, hipStream_t s) {
-    if (B == 0) return 0;
-    if (B > 0xFFFFFFFFull) return fail(BCHK_EINVAL, "batch too large");
+int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const double *d_y, size_t B,
+                uint8_t *d_res, double *d_l0, bchk_stats *d_st, hipStream_t s, const uint8_t *d_tx,
+                hipEvent_t wait_fast, hipEvent_t after_fast) {
     int rc;
-    if ((rc = c->ctrl.ensure(kCtrlBytes)) || (rc = ensure_heavy(c, B))) return rc;
+    if ((rc = P.ctrl.ensure(kCtrlBytes)) || (rc = ensure_heavy(P, B, s))) return rc;
     const bool fast = c->fast && c->use_fast;
-    if (fast && (rc = c->queue.ensure(B * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure_table(c))) return rc;
-    uint32_t *ctrl = (uint32_t *)c->ctrl.p;
+    if (fast && (rc = P.queue.ensure(B * sizeof(uint32_t)))) return rc;
+    uint32_t *ctrl = (uint32_t *)P.ctrl.p;
     SearchParams p{};
     p.y = d_y;
     p.res = d_res;
@@ -493,7 +541,11 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     p.t = c->t;
     p.J = c->J;
     p.variant = variant;
-    p.heavy_queue = (uint32_t *)c->heavy.p;
+    if (d_tx) {  // fused counters (zeroed by launch_search at allocation, then by every reduction)
+        p.tx = d_tx;
+        p.cnt = (unsigned long long *)c->cnt.p;
+    }
+    p.heavy_queue = (uint32_t *)P.heavy.p;
     p.heavy_tail = c->chunk_limit ? ctrl + kHeavyTail : nullptr;
     p.heavy_tail2 = ctrl + kHeavyTail2;
     p.heavy_head = ctrl + kHeavyHead;
@@ -517,10 +569,10 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     // analytic tail: the first pass hands its heavy codewords to the tail kernel (queue
     // l1q), which finishes most of them and hands the rest to the cooperative kernel
     const bool tail = c->analytic && c->ks.tail && p.heavy_tail && variant == BCHK_VARIANT_ANSWER;
-    if (tail && (rc = c->l1rec.ensure(B * sizeof(TailRec)))) return rc;
-    if (tail && B > c->l1q.cap / sizeof(uint32_t)) {
-        if ((rc = c->l1q.ensure(B * sizeof(uint32_t)))) return rc;
-        HIP_TRY(hipMemset(c->l1q.p, 0xFF, c->l1q.cap));  // empty slots (consumers restore them)
+    if (tail && (rc = P.l1rec.ensure(B * sizeof(TailRec)))) return rc;
+    if (tail && B > P.l1q.cap / sizeof(uint32_t)) {
+        if ((rc = P.l1q.ensure(B * sizeof(uint32_t)))) return rc;
+        HIP_TRY(hipMemsetAsync(P.l1q.p, 0xFF, P.l1q.cap, s));  // empty slots (consumers restore them)
     }
     // the tail kernel runs on the auxiliary stream, concurrently with the first pass
     const bool tconc = tail && c->tail_concurrent;
@@ -528,39 +580,42 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     // takes the long ones; the tail's own hand-offs to a second cooperative kernel on aux
     const bool hybrid = tail && !tconc && c->tail_min_bound > 0;
     const bool conc = c->coop_concurrent && p.heavy_tail && !tail;
-    hipStream_t cs = conc ? c->aux : s;  // the cooperative kernel's stream
+    hipStream_t cs = conc ? P.aux : s;  // the cooperative kernel's stream
     bchk_ctx::Ev ev{};
     if (c->profile) {
         for (auto &e : ev.e) HIP_TRY(hipEventCreate(&e));
+        ev.first = first;
         HIP_TRY(hipEventRecord(ev.e[0], s));
     }
     HIP_TRY(hipMemsetAsync(ctrl, 0, kCtrlBytes, s));
+    if (wait_fast) HIP_TRY(hipStreamWaitEvent(s, wait_fast, 0));
     if (fast) {
         SearchParams f = p;
 #ifdef BCHK_DIAG
         f.diag = p.diag + (size_t(1) << 20);  // fast-kernel stamps: second half of the buffer
 #endif
         f.qtail = ctrl;
-        f.queue_out = (uint32_t *)c->queue.p;
+        f.queue_out = (uint32_t *)P.queue.p;
         HIP_TRY(c->fast(f, c->lds_fast, s));
     }
+    if (after_fast) HIP_TRY(hipEventRecord(after_fast, s));
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[1], s));
     if (conc || tconc) {
-        HIP_TRY(hipEventRecord(c->ev_fork, s));
-        HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+        HIP_TRY(hipEventRecord(P.ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(P.aux, P.ev_fork, 0));
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[2], s));
     {
         SearchParams q = p;
         if (tail) {  // hand-offs (all to the front) into the tail kernel's queue
-            q.heavy_queue = (uint32_t *)c->l1q.p;
+            q.heavy_queue = (uint32_t *)P.l1q.p;
             q.heavy_tail = ctrl + kL1Tail;
             q.heavy_tail2 = ctrl + kL1Back;  // hybrid: loop bounds below heavy_big
             q.heavy_big = hybrid ? c->tail_min_bound : 0;
-            q.tail_rec = tconc ? nullptr : (TailRec *)c->l1rec.p;
+            q.tail_rec = tconc ? nullptr : (TailRec *)P.l1rec.p;
         }
         if (fast) {
-            q.queue = (const uint32_t *)c->queue.p;
+            q.queue = (const uint32_t *)P.queue.p;
             q.qcount = ctrl;
             q.heads = ctrl + 32;
             // every resident wave may take work; waves beyond the queue length exit at once
@@ -572,24 +627,24 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[3], s));
     SearchParams pc = p;  // the cooperative kernel's view of its producer
-    hipStream_t ts = (tconc || hybrid) ? c->aux : s;  // the tail kernel's stream
+    hipStream_t ts = (tconc || hybrid) ? P.aux : s;  // the tail kernel's stream
     if (hybrid) {
-        HIP_TRY(hipEventRecord(c->ev_fork, s));
-        HIP_TRY(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+        HIP_TRY(hipEventRecord(P.ev_fork, s));
+        HIP_TRY(hipStreamWaitEvent(P.aux, P.ev_fork, 0));
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[6], ts));
     if (tail) {
         SearchParams q = p;
-        q.queue = (const uint32_t *)c->l1q.p;
+        q.queue = (const uint32_t *)P.l1q.p;
         q.qcount = ctrl + kL1Tail;
         q.heads = ctrl + kTailHeads;
         q.exact_done = ctrl + kTailDone;
         q.analytic = 1;
         q.tail_stats = ctrl + kTailStats;
-        q.tail_rec = (TailRec *)c->l1rec.p;
+        q.tail_rec = (TailRec *)P.l1rec.p;
         if (tconc) {  // take the first pass's hand-offs as they come; recompute their state
             q.tail_rec = nullptr;
-            q.in_queue = (uint32_t *)c->l1q.p;
+            q.in_queue = (uint32_t *)P.l1q.p;
             q.in_tail = ctrl + kL1Tail;
             q.in_head = ctrl + kTailHeads;
             q.in_done = ctrl + kExactDone;
@@ -611,7 +666,7 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[7], ts));
     if (hybrid) {
         SearchParams ph = p;  // the first pass's short hand-offs: the back of l1q
-        ph.heavy_queue = (uint32_t *)c->l1q.p;
+        ph.heavy_queue = (uint32_t *)P.l1q.p;
         ph.heavy_tail = ctrl + kNoneTail;
         ph.heavy_head = ctrl + kNoneHead;
         ph.heavy_tail2 = ctrl + kL1Back;
@@ -620,15 +675,15 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         HIP_TRY(launch_coop(c->ks, ph, grid_coop, c->lds_coop, s));
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[5], s));
         // the tail kernel's hand-offs (rare) after it on aux, then s waits for aux
-        HIP_TRY(launch_coop(c->ks, pc, grid_coop, c->lds_coop, c->aux));
-        HIP_TRY(hipEventRecord(c->ev_join, c->aux));
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+        HIP_TRY(launch_coop(c->ks, pc, grid_coop, c->lds_coop, P.aux));
+        HIP_TRY(hipEventRecord(P.ev_join, P.aux));
+        HIP_TRY(hipStreamWaitEvent(s, P.ev_join, 0));
         if (c->profile) c->events.push_back(ev);
         return 0;
     }
     if (tconc) {  // the cooperative kernel (stream s) follows both
-        HIP_TRY(hipEventRecord(c->ev_join, c->aux));
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+        HIP_TRY(hipEventRecord(P.ev_join, P.aux));
+        HIP_TRY(hipStreamWaitEvent(s, P.ev_join, 0));
     }
     if (p.heavy_tail) {
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));
@@ -639,10 +694,51 @@ int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t
         HIP_TRY(hipEventRecord(ev.e[5], s));
     }
     if (conc) {
-        HIP_TRY(hipEventRecord(c->ev_join, cs));
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+        HIP_TRY(hipEventRecord(P.ev_join, cs));
+        HIP_TRY(hipStreamWaitEvent(s, P.ev_join, 0));
     }
     if (c->profile) c->events.push_back(ev);
+    return 0;
+}
+
+int launch_search(bchk_ctx *c, int variant, const double *d_y, size_t B, uint8_t *d_res,
+                  double *d_l0, bchk_stats *d_st, hipStream_t s, const uint8_t *d_tx = nullptr) {
+    if (B == 0) return 0;
+    if (B > 0xFFFFFFFFull) return fail(BCHK_EINVAL, "batch too large");
+    int rc;
+    if ((rc = ensure_table(c))) return rc;
+    int K = c->tail_diag_on ? 1 : std::max(1, c->npipes);
+    K = (int)std::min<size_t>((size_t)K, std::max<size_t>(1, B / c->pipe_min));
+    if ((rc = ensure_pipes(c, K))) return rc;
+    if (d_tx && !c->cnt.p) {  // fused counters: zeroed before any pipeline starts
+        if ((rc = c->cnt.ensure(size_t(kCntSlots) * kCntStride * 8))) return rc;
+        HIP_TRY(hipMemsetAsync(c->cnt.p, 0, c->cnt.cap, s));
+    }
+    c->last_pipes = K;
+    if (K == 1)
+        return launch_pipe(c, c->pipes[0], true, variant, d_y, B, d_res, d_l0, d_st, s, d_tx, nullptr, nullptr);
+    // sub-batches of whole 64-codeword chunks; pipe 0 on the caller's stream
+    const size_t n = (size_t)c->n;
+    const size_t chunk = ((B + K - 1) / K + 63) / 64 * 64;
+    HIP_TRY(hipEventRecord(c->ev_start, s));
+    hipEvent_t prev_fast = nullptr;
+    for (int k = 0; k < K; ++k) {
+        const size_t off = (size_t)k * chunk;
+        if (off >= B) break;
+        const size_t nb = std::min(chunk, B - off);
+        bchk_ctx::Pipe &P = c->pipes[k];
+        const hipStream_t ps = k ? P.s : s;
+        if (k) HIP_TRY(hipStreamWaitEvent(ps, c->ev_start, 0));
+        if ((rc = launch_pipe(c, P, k == 0, variant, d_y + off * n, nb, d_res + off * n, d_l0 ? d_l0 + off : nullptr,
+                              d_st ? d_st + off : nullptr, ps, d_tx ? d_tx + off * n : nullptr, prev_fast,
+                              k + 1 < K ? P.ev_fast : nullptr)))
+            return rc;
+        prev_fast = P.ev_fast;
+        if (k) {
+            HIP_TRY(hipEventRecord(P.ev_done, ps));
+            HIP_TRY(hipStreamWaitEvent(s, P.ev_done, 0));
+        }
+    }
     return 0;
 }
 
@@ -695,9 +791,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (hipMalloc(&c->d_tables, c->td.bytes) != hipSuccess ||
         hipMemcpy(c->d_tables, c->tables_host.data(), c->td.bytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        ensure_pipes(c, 1) != 0) {
         bchk_destroy(c);
         return fail(BCHK_EHIP, "device setup failed: %s", hipGetErrorString(hipGetLastError()));
     }
@@ -716,6 +810,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (const char *tc = getenv("BCHK_TAIL_CONCURRENT")) c->tail_concurrent = atoi(tc) != 0;
     if (const char *tb = getenv("BCHK_TAIL_BLOCKS")) c->tail_conc_blocks = std::max(1, atoi(tb));
     if (const char *tm = getenv("BCHK_TAIL_MIN_BOUND")) c->tail_min_bound = strtoull(tm, nullptr, 10);
+    if (const char *np = getenv("BCHK_PIPES")) c->npipes = std::max(1, std::min(8, atoi(np)));
+    if (const char *pm = getenv("BCHK_PIPE_MIN")) c->pipe_min = std::max<size_t>(64, strtoull(pm, nullptr, 10));
     c->lds_coop = tb + c->ks.coop_bytes;
     // one cooperative workgroup per CU by default (LDS sized past half the CU's 160 KB):
     // a heavy codeword's 16 waves then own the CU's four SIMDs, which shortens the longest
@@ -751,12 +847,10 @@ void bchk_destroy(bchk_ctx *c) {
     if (!c) return;
     for (auto &e : c->events)
         for (auto &x : e.e) (void)hipEventDestroy(x);
-    c->queue.release();
-    c->l1q.release();
-    c->l1rec.release();
+    release_pipes(c);
     c->tdiag.release();
-    c->heavy.release();
-    c->ctrl.release();
+    c->cnt.release();
+    for (DevBuf *b : {&c->gtx, &c->gy, &c->gres, &c->gst, &c->gcnt, &c->gflags}) b->release();
     c->y.release();
     c->res.release();
     c->l0.release();
@@ -766,9 +860,6 @@ void bchk_destroy(bchk_ctx *c) {
     c->ok.release();
     if (c->d_tables) (void)hipFree(c->d_tables);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->aux) (void)hipStreamDestroy(c->aux);
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -862,6 +953,16 @@ int bchk_alg_decode_host(bchk_ctx *c, const uint8_t *words, const uint32_t *synd
     HIP_TRY(hipMemcpyAsync(answers, c->res.p, N * n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(ok, c->ok.p, N, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int bchk_decode_count_device(bchk_ctx *c, const double *d_y, const uint8_t *d_tx, size_t B, uint8_t *d_res,
+                             double *d_l0, bchk_stats *d_st, uint64_t *d_out6, void *stream) {
+    if (!c || (B && (!d_y || !d_tx || !d_res || !d_out6))) return fail(BCHK_EINVAL, "NULL argument");
+    if (B == 0) return 0;
+    const hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (int rc = launch_search(c, BCHK_VARIANT_ANSWER, d_y, B, d_res, d_l0, d_st, s, d_tx)) return rc;
+    HIP_TRY(launch_cnt_reduce((unsigned long long *)c->cnt.p, (unsigned long long *)d_out6, s));
     return 0;
 }
 
@@ -1001,6 +1102,118 @@ int bchk_generate_host(const bchk_ctx *c, double snr_db, size_t B, uint64_t *rng
     return 0;
 }
 
+// On-GPU channel (bchk_channel.hip): words [word0, word0 + B) of the counter-based stream
+// `seed` at Eb/N0 snr_db (sd as src/dataForPlot.cpp:45), tx and y written on device.
+int bchk_generate_device(bchk_ctx *c, double snr_db, size_t B, uint64_t seed, uint64_t word0, uint8_t *d_tx,
+                         double *d_y, void *stream) {
+    if (!c || (B && (!d_tx || !d_y))) return fail(BCHK_EINVAL, "NULL argument");
+    if (B > 0xFFFFFFFFull) return fail(BCHK_EINVAL, "batch too large");
+    if (B == 0) return 0;
+    ChanParams cp{};
+    cp.tx = d_tx;
+    cp.y = d_y;
+    cp.word0 = word0;
+    cp.count = (uint32_t)B;
+    cp.n = c->n;
+    cp.k = c->k;
+    cp.seed_lo = (uint32_t)seed;
+    cp.seed_hi = (uint32_t)(seed >> 32);
+    cp.sd = sweep_sigma(c, snr_db);
+    for (size_t j = 0; j < c->g.size(); ++j)
+        if (c->g[j]) cp.g[j >> 6] |= 1ull << (j & 63);
+    HIP_TRY(launch_channel(cp, stream ? (hipStream_t)stream : c->stream));
+    return 0;
+}
+
+// fun() (src/dataForPlot.cpp:16-74) with the words generated on the GPU (statistically the
+// reference's stream, not bit-exactly) and the counters fused into the decode: Eb/N0 from 0
+// to max_snr in steps of 0.5, each point until p words or e frame errors -- the e-th error
+// cut exactly in word order (the batch that reaches it is decoded again with per-word
+// stats and counted up to that word). CSV as bchk_sweep; seconds = wall time of the sweep,
+// words = words decoded (including the re-decoded tail batches once).
+int bchk_sweep_device(bchk_ctx *c, long p, long e, double max_snr, uint64_t seed, size_t batch, char *csv,
+                      size_t cap, double *seconds, uint64_t *words) {
+    if (!c || !csv || cap == 0) return fail(BCHK_EINVAL, "NULL argument");
+    if (p <= 0 || e <= 0) return fail(BCHK_EINVAL, "p and e must be positive");
+    const size_t n = c->n;
+    const size_t B = batch ? batch : (size_t(1) << 20);
+    int rc;
+    if ((rc = c->gtx.ensure(B * n)) || (rc = c->gy.ensure(B * n * sizeof(double))) || (rc = c->gres.ensure(B * n)) ||
+        (rc = c->gst.ensure(B * sizeof(bchk_stats))) || (rc = c->gcnt.ensure(16 * sizeof(uint64_t))) ||
+        (rc = c->gflags.ensure(B)))
+        return rc;
+    const hipStream_t s = c->stream;
+    HIP_TRY(hipMemsetAsync(c->gres.p, 0, B * n, s));
+    const auto t0 = std::chrono::steady_clock::now();
+    std::ostringstream out;
+    long count = 0, countErr = 0;
+    long long countE = 0;  // never reset between points, as src/dataForPlot.cpp:20,61
+    unsigned long D = 0, Cc = 0, Ss = 0, wordCount = 0;
+    uint64_t word = 0, decoded = 0;
+    std::vector<uint8_t> flags;
+    uint64_t h[6];
+    uint64_t *d6 = (uint64_t *)c->gcnt.p;
+    for (double stnr = 0.0; stnr <= max_snr; stnr += 0.5) {
+        while (count < p && countErr < e) {
+            const size_t nb = std::min<size_t>(B, (size_t)(p - count));
+            if ((rc = bchk_generate_device(c, stnr, nb, seed, word, (uint8_t *)c->gtx.p, (double *)c->gy.p, s)))
+                return rc;
+            HIP_TRY(hipMemsetAsync(d6, 0, 6 * sizeof(uint64_t), s));
+            if ((rc = bchk_decode_count_device(c, (const double *)c->gy.p, (const uint8_t *)c->gtx.p, nb,
+                                               (uint8_t *)c->gres.p, nullptr, nullptr, d6, s)))
+                return rc;
+            HIP_TRY(hipMemcpyAsync(h, d6, sizeof h, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            decoded += nb;
+            size_t used = nb;
+            if (countErr + (long)h[0] >= e) {  // the e-th error falls in this batch: cut there
+                if ((rc = launch_search(c, BCHK_VARIANT_ANSWER, (const double *)c->gy.p, nb, (uint8_t *)c->gres.p,
+                                        nullptr, (bchk_stats *)c->gst.p, s)))
+                    return rc;
+                HIP_TRY(launch_frame_errors((const uint8_t *)c->gtx.p, (const uint8_t *)c->gres.p, (uint32_t)nb,
+                                            (int)n, (uint8_t *)c->gflags.p, s));
+                flags.resize(nb);
+                HIP_TRY(hipMemcpyAsync(flags.data(), c->gflags.p, nb, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                long need = e - countErr;
+                used = nb;
+                for (size_t w = 0; w < nb; ++w)
+                    if (flags[w] && --need == 0) {
+                        used = w + 1;
+                        break;
+                    }
+                HIP_TRY(hipMemsetAsync(d6, 0, 6 * sizeof(uint64_t), s));
+                HIP_TRY(launch_count(c->n, (const uint8_t *)c->gtx.p, (const uint8_t *)c->gres.p,
+                                     (const bchk_stats *)c->gst.p, (uint32_t)used, d6, s));
+                HIP_TRY(hipMemcpyAsync(h, d6, sizeof h, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                decoded += nb;
+            }
+            countErr += (long)h[0];
+            countE += (long long)h[1];
+            D += h[2];
+            Cc += h[3];
+            Ss += h[4];
+            count += (long)used;
+            wordCount += used;
+            word += used;
+        }
+        out << stnr << "," << ((double)countErr) / count << "," << ((double)countE) / count / (long)n << ","
+            << ((double)D) / wordCount << "," << ((double)Cc) / wordCount << "," << ((double)Ss) / wordCount
+            << "\n";
+        D = Cc = Ss = 0;
+        wordCount = 0;
+        count = 0, countErr = 0;
+    }
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (seconds) *seconds = secs;
+    if (words) *words = decoded;
+    const std::string str = out.str();
+    if (str.size() + 1 > cap) return fail(BCHK_EINVAL, "csv buffer too small (%zu needed)", str.size() + 1);
+    memcpy(csv, str.c_str(), str.size() + 1);
+    return 0;
+}
+
 int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t *rng_state, uint64_t seed,
                size_t batch, char *csv, size_t cap) {
     if (!c || !csv || cap == 0) return fail(BCHK_EINVAL, "NULL argument");
@@ -1094,7 +1307,7 @@ int bchk_profile_read_stages(bchk_ctx *c, double *ms4, uint64_t *launches) {
             HIP_TRY(hipEventElapsedTime(&ms, e.e[2 * k], e.e[2 * k + 1]));
             c->prof_ms[k] += ms;
         }
-        c->prof_launches += 1;
+        c->prof_launches += e.first ? 1 : 0;  // per call: a call's pipelines add up
         for (auto &x : e.e) (void)hipEventDestroy(x);
     }
     c->events.clear();
@@ -1131,7 +1344,8 @@ int bchk_tail_diag_read(bchk_ctx *c, uint64_t *out, size_t items, uint64_t *coun
     *count = 0;
     if (!c->tdiag.p) return 0;
     uint32_t n = 0;
-    HIP_TRY(hipMemcpy(&n, (uint32_t *)c->ctrl.p + kTailStats + 16, 4, hipMemcpyDeviceToHost));
+    if (c->pipes.empty() || !c->pipes[0].ctrl.p) return 0;
+    HIP_TRY(hipMemcpy(&n, (uint32_t *)c->pipes[0].ctrl.p + kTailStats + 16, 4, hipMemcpyDeviceToHost));
     const size_t m = std::min<size_t>({items, (size_t)n, c->tdiag.cap / 64});
     HIP_TRY(hipMemcpy(out, c->tdiag.p, m * 64, hipMemcpyDeviceToHost));
     *count = n;
@@ -1148,15 +1362,23 @@ int bchk_tail_stats(bchk_ctx *c, uint64_t *out6) {
 
 int bchk_path_counts(bchk_ctx *c, uint64_t *to_exact, uint64_t *to_coop) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
+    // the last call's counts, summed over its pipelines (a pipeline the call did not use
+    // still holds an earlier call's: only the first npipes_used are read)
     uint64_t v[2] = {0, 0};
-    if (c->ctrl.p) {
+    c->last_tail = 0;
+    for (auto &x : c->last_tail_stats) x = 0;
+    for (int k = 0; k < c->last_pipes && k < (int)c->pipes.size(); ++k) {
+        const bchk_ctx::Pipe &P = c->pipes[k];
+        if (!P.ctrl.p) continue;
         std::vector<uint32_t> h(kCtrlBytes / 4);
-        HIP_TRY(hipMemcpyAsync(h.data(), c->ctrl.p, kCtrlBytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(h.data(), P.ctrl.p, kCtrlBytes, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        v[0] = h[0];
-        v[1] = (uint64_t)h[kHeavyTail] + h[kHeavyTail2];
-        c->last_tail = h[kL1Tail];
-        for (int k = 0; k < 6; ++k) c->last_tail_stats[k] = h[kTailStats + k];
+        v[0] += h[0];
+        v[1] += (uint64_t)h[kHeavyTail] + h[kHeavyTail2];
+        c->last_tail += h[kL1Tail];
+        for (int q = 0; q < 6; ++q)
+            c->last_tail_stats[q] = q == 5 ? std::max<uint64_t>(c->last_tail_stats[q], h[kTailStats + q])
+                                           : c->last_tail_stats[q] + h[kTailStats + q];
     }
     if (to_exact) *to_exact = v[0];
     if (to_coop) *to_coop = v[1];

@@ -486,13 +486,29 @@ __device__ __forceinline__ void write_outputs(const SearchState<Geo<M>::NW> &S, 
     const uint64_t decodes = S.i_end;
     const uint64_t iters = S.returned ? S.i_end - 1 : S.i_end;
     const uint64_t pro = word_variant ? (uint64_t)(2 * N + 1) : 0ull;  // :221-224
-    if (S.accepted) {
+    uint32_t bit_errors = 0;
 #pragma unroll
-        for (int s = 0; s < NW; ++s) {
-            const int pos = lane + 64 * s;
-            if (pos < N)
-                p.res[(size_t)cw * N + pos] = (uint8_t)(((P.yH.w[s] ^ S.best.w[s]) >> lane) & 1ull);
+    for (int s = 0; s < NW; ++s) {
+        const int pos = lane + 64 * s;
+        uint8_t x = 0;
+        if (S.accepted) {
+            x = (uint8_t)(((P.yH.w[s] ^ S.best.w[s]) >> lane) & 1ull);
+            if (pos < N) p.res[(size_t)cw * N + pos] = x;
+        } else if (p.cnt && pos < N) {
+            x = p.res[(size_t)cw * N + pos];  // not accepted: the row stays the caller's
         }
+        if (p.cnt) bit_errors += (uint32_t)__popcll(ballot(pos < N && x != p.tx[(size_t)cw * N + pos]));
+    }
+    if (p.cnt && lane == 0) {  // src/dataForPlot.cpp:55-74
+        unsigned long long *c = p.cnt + (size_t)(cw % (uint32_t)kCntSlots) * kCntStride;
+        if (bit_errors) {
+            atomicAdd(c + 0, 1ull);
+            atomicAdd(c + 1, (unsigned long long)bit_errors);
+        }
+        atomicAdd(c + 2, (unsigned long long)decodes);
+        atomicAdd(c + 3, (unsigned long long)(pro + iters * (uint64_t)(N + 6) + S.jsteps + S.impr));
+        atomicAdd(c + 4, (unsigned long long)(pro + iters * (uint64_t)(N + 1) + S.jsteps));
+        atomicAdd(c + 5, 1ull);
     }
     if (lane == 0) {
         if (p.l0) p.l0[cw] = S.l0;
@@ -1424,6 +1440,7 @@ kaneko_search_kernel(SearchParams p) {
                 if (lane == 0) cw = tail_dequeue(p);
                 cw = (uint32_t)__shfl((int)cw, 0, 64);
                 if (cw == kEmptySlot) break;
+                if (cw >= p.count) continue;  // never a valid slot value
                 search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, 0u);
                 ++ndone;
             }
@@ -1455,7 +1472,9 @@ kaneko_search_kernel(SearchParams p) {
             ++exhausted;
             continue;
         }
-        search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, p.queue[item], lane, an, item);
+        const uint32_t cw = p.queue[item];
+        if (cw < p.count)  // never otherwise: no access outside the batch
+            search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item);
         ++ndone;
     }
     wave_done(p, lane, ndone);
@@ -1656,6 +1675,7 @@ kaneko_coop_kernel(SearchParams p) {
         __syncthreads();
         const uint32_t item = ctl->item;
         if (item == kEmptySlot) return;
+        if (item >= p.count) continue;  // never a valid slot value: no access outside the batch
         const uint32_t cw = item;
 #ifdef BCHK_DIAG
         const uint32_t drec = ctl->drec;  // this codeword's diagnostic record
@@ -1879,6 +1899,37 @@ __global__ void __launch_bounds__(256) alg_decode_kernel(AlgParams p) {
 // One wave per 64 rows: the rows' bytes are read as 16-B vectors (the 64-row block of
 // 64n bytes is contiguous and 16-B aligned when the arrays are), differing bytes -- rare at
 // the SNRs of interest -- are tallied per row in LDS, then lane r owns row r.
+// The fused counters' partial slots into the caller's totals (one block), slots zeroed for
+// the next call.
+__global__ void __launch_bounds__(256) cnt_reduce_kernel(unsigned long long *cnt, unsigned long long *out6) {
+    __shared__ unsigned long long part[6][4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
+    for (int sl = threadIdx.x; sl < kCntSlots; sl += 256) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            c[k] += cnt[(size_t)sl * kCntStride + k];
+            cnt[(size_t)sl * kCntStride + k] = 0ull;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c[k] += (unsigned long long)__shfl_xor((long long)c[k], o, 64);
+        if (lane == 0) part[k][wid] = c[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        out6[k] += part[k][0] + part[k][1] + part[k][2] + part[k][3];
+    }
+}
+
+hipError_t launch_cnt_reduce(unsigned long long *cnt, unsigned long long *out6, hipStream_t s) {
+    hipLaunchKernelGGL(cnt_reduce_kernel, dim3(1), dim3(256), 0, s, cnt, out6);
+    return hipGetLastError();
+}
+
 template <int N>
 __global__ void __launch_bounds__(256) count_kernel(const uint8_t *tx, const uint8_t *res,
                                                     const bchk_stats *st, uint32_t B,

@@ -50,5 +50,11 @@ constexpr int kCoopThreads = 1024;
 hipError_t launch_alg(const KernelSet &k, const AlgParams &p, size_t lds, hipStream_t s);
 hipError_t launch_count(int n, const uint8_t *tx, const uint8_t *res, const bchk_stats *st,
                         uint32_t B, uint64_t *out6, hipStream_t s);
+// on-GPU channel words (bchk_channel.hip) and per-word frame-error flags (tx != res)
+hipError_t launch_channel(const ChanParams &cp, hipStream_t s);
+hipError_t launch_frame_errors(const uint8_t *tx, const uint8_t *res, uint32_t B, int n, uint8_t *flags,
+                               hipStream_t s);
+// the fused counters (SearchParams::cnt) into out6, slots zeroed
+hipError_t launch_cnt_reduce(unsigned long long *cnt, unsigned long long *out6, hipStream_t s);
 
 }  // namespace bchk

@@ -354,7 +354,7 @@ def test_long_code_sort_and_first_pattern_edge_rows(m, t):
     y[6, n - 1] = -y[6, 0] * (1 + 2.0 ** -50)     # prefix tie at the ends of the order
     F = load()
     for J in (15, -1):
-        for path in ("fast+exact+coop", "exact-only", "coop-heavy"):
+        for path in ("fast+exact+tail", "exact-only", "coop-heavy"):
             d = dec(m, t, J=J, path=path)
             d.set_max_decodes(1 << 16)
             res, l0, st = d.decode(y)
@@ -370,7 +370,7 @@ def test_long_code_batch_paths_agree_and_sample_matches_oracle():
     # BCH(255,139,31) at a batch large enough to fill the chip: all execution paths agree,
     # and a sample matches the oracle (uncapped loop, the shipped semantics)
     o = Oracle(8, 15)
-    ds = [dec(8, 15, J=-1, path=p) for p in ("fast+exact+coop", "exact-only", "coop-heavy")]
+    ds = [dec(8, 15, J=-1, path=p) for p in ("fast+exact+tail", "exact-only", "coop-heavy")]
     _, y, _ = ds[0].generate(6.5, 1 << 15, seed=41)
     a = ds[0].decode(y)
     for d in ds[1:]:
@@ -383,3 +383,90 @@ def test_long_code_batch_paths_agree_and_sample_matches_oracle():
     idx = np.random.default_rng(3).choice(light, 200, replace=False)
     r2, l2, s2, a2 = o.kaneko_batch(y[idx], J=-1)
     check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, a[0][idx], a[1][idx], a[2][idx])
+
+
+@pytest.mark.parametrize("exec_path", list(PATHS))
+@pytest.mark.parametrize("m,t,J,snr", [(6, 6, 15, 4.0), (6, 6, 15, 6.0), (6, 6, -1, 5.0), (5, 3, 15, 2.0),
+                                       (8, 15, 15, 7.0)])
+def test_fused_counters_equal_decode_then_count(m, t, J, snr, exec_path):
+    # bchk_decode_count_device (counters inside every kernel that finishes a codeword) against
+    # bchk_decode_device + bchk_count_device, and against numpy on the host copies; rows the
+    # decoder never accepts keep the caller's contents (here: a nonzero fill) in both
+    import torch
+    if m >= 7 and exec_path != "fast+exact+tail":
+        pytest.skip("long codes: one path")
+    d = dec(m, t, J=J, path=exec_path) if m <= 6 else dec(m, t, J=J)
+    B = 1 << 14
+    tx, y, _ = d.generate(snr, B, seed=17)
+    n = d.n
+    dy = torch.from_numpy(y).cuda()
+    dtx = torch.from_numpy(tx).cuda()
+    fill = (np.arange(B * n, dtype=np.uint64).reshape(B, n) % 3 == 0).astype(np.uint8)
+    outs = []
+    for fused in (False, True):
+        dres = torch.from_numpy(fill.copy()).cuda()
+        dl0 = torch.zeros(B, dtype=torch.float64, device="cuda")
+        dst = torch.zeros((B, 56), dtype=torch.uint8, device="cuda")
+        c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
+        c6[:] = torch.tensor([3, 5, 7, 11, 13, 17])  # the calls add to what is there
+        if fused:
+            d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), 0,
+                                  c6.data_ptr())
+        else:
+            d.decode_device(dy.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), dst.data_ptr())
+            d.count_device(dtx.data_ptr(), dres.data_ptr(), dst.data_ptr(), B, c6.data_ptr())
+        d.sync()
+        outs.append((dres.cpu().numpy(), dl0.cpu().numpy(), c6.cpu().numpy(), dst.cpu().numpy()))
+    (r0, l0a, c0, st0), (r1, l0b, c1, _) = outs
+    np.testing.assert_array_equal(r0, r1)
+    np.testing.assert_array_equal(l0a.view(np.uint64), l0b.view(np.uint64))
+    np.testing.assert_array_equal(c0, c1)
+    st = st0.view(load().STATS_DTYPE).reshape(B)
+    err = (r0 != tx).sum(axis=1)
+    want = [3 + int((err > 0).sum()), 5 + int(err.sum()), 7 + int(st["decodes"].sum()),
+            11 + int(st["comparisons"].sum()), 13 + int(st["sums"].sum()), 17 + B]
+    np.testing.assert_array_equal(c1, want)
+    # a second fused call adds the same counts again (the partial slots were zeroed)
+    dres = torch.from_numpy(fill.copy()).cuda()
+    c6 = torch.from_numpy(c1.copy()).cuda()
+    d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), 0, 0, c6.data_ptr())
+    d.sync()
+    np.testing.assert_array_equal(c6.cpu().numpy(), 2 * c1 - np.array([3, 5, 7, 11, 13, 17]))
+
+
+@pytest.mark.parametrize("m,t,J,snr", [(6, 6, 15, 4.0), (6, 6, -1, 5.0), (5, 3, 15, 2.0), (8, 15, 15, 7.0)])
+def test_sub_batch_pipelines_match_one_pipeline(m, t, J, snr):
+    # a call split over 3 pipelines (sub-batches on their own streams, each fast kernel after
+    # the previous one) gives the single pipeline's results, counters and path counts
+    import torch
+    F = load()
+    old = {k: os.environ.get(k) for k in ("BCHK_PIPES", "BCHK_PIPE_MIN")}
+    try:
+        os.environ["BCHK_PIPES"], os.environ["BCHK_PIPE_MIN"] = "3", "4096"
+        multi = F.KanekoKernelProcessor(m, t, J=J)
+        os.environ["BCHK_PIPES"] = "1"
+        one = F.KanekoKernelProcessor(m, t, J=J)
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+    B = 3 * 4096 + 1000  # ragged last sub-batch
+    tx, y, _ = one.generate(snr, B, seed=23)
+    a = one.decode(y)
+    b = multi.decode(y)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+    np.testing.assert_array_equal(a[2], b[2])
+    assert one.path_counts() == multi.path_counts()
+    assert one.tail_count() == multi.tail_count()
+    dy, dtx = torch.from_numpy(y).cuda(), torch.from_numpy(tx).cuda()
+    outs = []
+    for d in (one, multi):
+        dres = torch.zeros((B, d.n), dtype=torch.uint8, device="cuda")
+        c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
+        d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), 0, 0, c6.data_ptr())
+        d.sync()
+        outs.append((dres.cpu().numpy(), c6.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
