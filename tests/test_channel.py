@@ -30,7 +30,7 @@ def test_channel_words_are_codewords_with_gaussian_noise(m, t, snr):
     import torch
     d = load().KanekoKernelProcessor(m, t, J=15)
     n, B = d.n, 20000
-    g = np.array(d.generator(), np.uint8)
+    g = np.array(d.g, np.uint8)
     dtx = torch.zeros((B, n), dtype=torch.uint8, device="cuda")
     dy = torch.zeros((B, n), dtype=torch.float64, device="cuda")
     d.generate_device(snr, B, dtx.data_ptr(), dy.data_ptr(), seed=5, word0=123)
