@@ -372,7 +372,7 @@ struct bchk_ctx {
     bool use_fast = true;
     size_t lds_fast = 0, lds_coop = 0;
     int grid_coop = 0, grid_coop_tab = 0;
-    uint32_t chunk_limit = 4;  // exact steps before a hand-off (measured best at 4-6 dB)
+    uint32_t chunk_limit = 8;  // exact steps before a hand-off (measured best over 4-6 dB, J = 15 / inf)
     DevBuf diag;
     // One decode pipeline per sub-batch: its work queues, control words (one 128-B line
     // each) and streams. A call splits a large batch over npipes pipelines, each on its own
