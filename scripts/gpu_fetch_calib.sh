@@ -1,7 +1,6 @@
 #!/bin/bash
 # FETCH_SIZE calibration (scripts/fetch_calib.hip): timing run, then one FETCH_SIZE pass.
-# The binary is built on the CPU side: hipcc --offload-arch=gfx950 -O3 scripts/fetch_calib.hip
-#   -o scripts/fetch_calib
+# The binary is built on the CPU side first: make -C polar-codes-with-bch-kernel_amd fetch_calib
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
