@@ -58,6 +58,14 @@ struct SearchParams {
     uint32_t *heads;
     uint32_t *qtail;       // fast path: append unresolved codewords here (with queue_out)
     uint32_t *queue_out;
+    // fast path, two-ended queue (null: all at the front): codewords likely to be heavy
+    // (the hard decision does not decode) take slots 0, 1, ... (qfront), the others slots
+    // count-1, count-2, ... (qback); *qtail stays the total. The first pass reads items
+    // below *qfront_n from the front, the rest from the back, so it starts the likely heavy
+    // codewords first and hands them to a concurrent tail kernel early.
+    uint32_t *qfront;
+    uint32_t *qback;
+    const uint32_t *qfront_n;
     // heavy codewords: the wave kernel hands a codeword still running after chunk_limit
     // steps of 64 patterns to the cooperative kernel, which may run concurrently with it
     // (heavy_tail == null disables the hand-off). Longest-first: codewords whose loop bound

@@ -405,7 +405,22 @@ kaneko_fast_kernel(SearchParams p) {
     // ---- everything else goes to the exact wave-per-codeword path
     const bool unres = live && state == 0;
     const uint64_t um = ballot(unres);
-    if (um) {
+    if (um && p.qfront) {
+        // likely heavy: the hard decision itself does not decode (nor is it a codeword)
+        const bool hv = unres && !bad && !ok0 && !zero0;
+        const uint64_t hm = ballot(hv), om = um & ~hm;
+        const uint64_t below = (1ull << lane) - 1ull;
+        uint32_t bf = 0, bb = 0;
+        if (lane == 0) {
+            if (hm) bf = atomicAdd(p.qfront, (uint32_t)__popcll(hm));
+            if (om) bb = atomicAdd(p.qback, (uint32_t)__popcll(om));
+            atomicAdd(p.qtail, (uint32_t)__popcll(um));
+        }
+        bf = (uint32_t)__shfl((int)bf, 0, 64);
+        bb = (uint32_t)__shfl((int)bb, 0, 64);
+        if (hv) p.queue_out[bf + (uint32_t)__popcll(hm & below)] = cw;
+        else if (unres) p.queue_out[p.count - 1u - (bb + (uint32_t)__popcll(om & below))] = cw;
+    } else if (um) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(p.qtail, (uint32_t)__popcll(um));
         base = (uint32_t)__shfl((int)base, 0, 64);

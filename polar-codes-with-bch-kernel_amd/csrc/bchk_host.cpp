@@ -401,7 +401,8 @@ struct bchk_ctx {
     uint64_t last_tail_stats[6] = {0, 0, 0, 0, 0, 0};
     bool tail_diag_on = false;     // BCHK_TAIL_DIAG=1: per-codeword tail timing records
     bool tail_concurrent = false;  // BCHK_TAIL_CONCURRENT=1: the tail kernel beside the first pass
-    int tail_conc_blocks = 256;    // blocks of the concurrent tail kernel (one per CU)
+    int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
+    bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
     // hybrid tail: a first-pass hand-off whose loop bound is below this goes to a cooperative
     // kernel running beside the tail kernel instead (0: every hand-off to the tail kernel)
     uint64_t tail_min_bound = 0;
@@ -435,12 +436,13 @@ int sigma_s2(int k, int n, double snr_db, double *sd) {
 // exact kernel has finished (13-20), diagnostic record count (21), the first pass's
 // hand-offs to the analytic tail kernel (22), its 8 per-XCD heads (23-30) and finished
 // counts (31-38), its outcome counters (39), an always-empty queue tail and head (40, 41),
-// the hybrid tail's back-queue tail and head (42, 43); zeroed by one memset per decode call
-constexpr size_t kCtrlBytes = 44 * 128;
+// the hybrid tail's back-queue tail and head (42, 43), the fast path's front / back queue
+// counts (44, 45); zeroed by one memset per decode call
+constexpr size_t kCtrlBytes = 46 * 128;
 constexpr int kHeavyTail = 32 * 9, kHeavyHead = 32 * 10, kHeavyTail2 = 32 * 11,
               kHeavyHead2 = 32 * 12, kExactDone = 32 * 13, kL1Tail = 32 * 22, kTailHeads = 32 * 23,
               kTailDone = 32 * 31, kTailStats = 32 * 39, kNoneTail = 32 * 40, kNoneHead = 32 * 41,
-              kL1Back = 32 * 42, kL1BackHead = 32 * 43;
+              kL1Back = 32 * 42, kL1BackHead = 32 * 43, kQFront = 32 * 44, kQBack = 32 * 45;
 #ifdef BCHK_DIAG
 constexpr int kDiagCount = 32 * 21;
 #endif
@@ -596,6 +598,10 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
 #endif
         f.qtail = ctrl;
         f.queue_out = (uint32_t *)P.queue.p;
+        if (c->heavy_first && c->m <= 6) {  // the lane fast kernel (m >= 7: the first kernel)
+            f.qfront = ctrl + kQFront;
+            f.qback = ctrl + kQBack;
+        }
         HIP_TRY(c->fast(f, c->lds_fast, s));
     }
     if (after_fast) HIP_TRY(hipEventRecord(after_fast, s));
@@ -612,12 +618,13 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             q.heavy_tail = ctrl + kL1Tail;
             q.heavy_tail2 = ctrl + kL1Back;  // hybrid: loop bounds below heavy_big
             q.heavy_big = hybrid ? c->tail_min_bound : 0;
-            q.tail_rec = tconc ? nullptr : (TailRec *)P.l1rec.p;
+            q.tail_rec = (TailRec *)P.l1rec.p;
         }
         if (fast) {
             q.queue = (const uint32_t *)P.queue.p;
             q.qcount = ctrl;
             q.heads = ctrl + 32;
+            if (c->heavy_first && c->m <= 6) q.qfront_n = ctrl + kQFront;
             // every resident wave may take work; waves beyond the queue length exit at once
             HIP_TRY(launch_search(c->ks, q, grid, c->lds, s));
         } else {
@@ -642,8 +649,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
         q.analytic = 1;
         q.tail_stats = ctrl + kTailStats;
         q.tail_rec = (TailRec *)P.l1rec.p;
-        if (tconc) {  // take the first pass's hand-offs as they come; recompute their state
-            q.tail_rec = nullptr;
+        if (tconc) {  // take the first pass's hand-offs as they come, with their state
             q.in_queue = (uint32_t *)P.l1q.p;
             q.in_tail = ctrl + kL1Tail;
             q.in_head = ctrl + kTailHeads;
@@ -810,6 +816,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (const char *tc = getenv("BCHK_TAIL_CONCURRENT")) c->tail_concurrent = atoi(tc) != 0;
     if (const char *tb = getenv("BCHK_TAIL_BLOCKS")) c->tail_conc_blocks = std::max(1, atoi(tb));
     if (const char *tm = getenv("BCHK_TAIL_MIN_BOUND")) c->tail_min_bound = strtoull(tm, nullptr, 10);
+    if (const char *hf = getenv("BCHK_HEAVY_FIRST")) c->heavy_first = atoi(hf) != 0;
     if (const char *np = getenv("BCHK_PIPES")) c->npipes = std::max(1, std::min(8, atoi(np)));
     if (const char *pm = getenv("BCHK_PIPE_MIN")) c->pipe_min = std::max<size_t>(64, strtoull(pm, nullptr, 10));
     c->lds_coop = tb + c->ks.coop_bytes;

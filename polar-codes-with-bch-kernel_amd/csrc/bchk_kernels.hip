@@ -1163,6 +1163,28 @@ __device__ void an_replay(SearchState<1> &S, const Prep<M, TMAX> &P, const AnWav
     S.done = true;
 }
 
+// A TailRec crosses XCDs (L2s not coherent) when the tail kernel runs beside the first
+// pass: written and read as device-scope relaxed atomics, and the writer waits for its
+// stores before it publishes the queue slot.
+static_assert(sizeof(TailRec) % 8 == 0, "TailRec as u64 words");
+__device__ __forceinline__ void tail_rec_store(TailRec *dst, const TailRec &r) {
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(&r);
+    uint64_t *d = reinterpret_cast<uint64_t *>(dst);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(TailRec) / 8); ++i)
+        __hip_atomic_store(d + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ TailRec tail_rec_load(const TailRec *src) {
+    TailRec r;
+    uint64_t *d = reinterpret_cast<uint64_t *>(&r);
+    const uint64_t *s = reinterpret_cast<const uint64_t *>(src);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(TailRec) / 8); ++i)
+        d[i] = __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return r;
+}
+
 // ------------------------------------------------ wave-per-codeword search
 // 64 consecutive test patterns per step, acceptance in pattern order. A codeword still
 // running after p.chunk_limit steps finishes through the analytic tail (above) or is handed
@@ -1219,8 +1241,8 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     uint32_t chunks = 0;
     uint64_t base00 = 0;
     if constexpr (AN && G == 1) {
-        if (p.tail_rec && p.queue) {  // resume where the first pass handed this codeword off
-            const TailRec r = p.tail_rec[item];
+        if (p.tail_rec && (p.queue || p.in_queue)) {  // resume where the first pass handed it off
+            const TailRec r = tail_rec_load(p.tail_rec + item);
             S.l0 = r.l0;
             S.bound = r.bound;
             S.jsteps = r.jsteps;
@@ -1311,7 +1333,7 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
                                 r.m0 = S.m0;
                                 r.chunks = chunks;
                                 r.flags = (S.firstOK ? 1u : 0u) | (S.accepted ? 2u : 0u);
-                                p.tail_rec[k] = r;
+                                tail_rec_store(p.tail_rec + k, r);  // complete before the slot store
                             }
                         }
                     } else {
@@ -1384,7 +1406,7 @@ __device__ __forceinline__ void wave_done(const SearchParams &p, int lane, uint3
 // tail, then stores the codeword; consumers restore empty slots), kEmptySlot once the
 // first pass has finished (its per-XCD done counts reach *in_total) and no ticket is left.
 // Every wait is bounded (a logic error ends the wave instead of hanging it).
-__device__ uint32_t tail_dequeue(const SearchParams &p) {
+__device__ uint32_t tail_dequeue(const SearchParams &p, uint32_t &item) {
     constexpr uint32_t kTailSpin = 1u << 24;  // ~1 s of polling: a guard against logic errors
     const uint32_t total = p.in_total ? *p.in_total : p.count;
     const uint32_t k = atomicAdd(p.in_head, 1u);
@@ -1395,6 +1417,7 @@ __device__ uint32_t tail_dequeue(const SearchParams &p) {
                 const uint32_t cw = ld_rlx(slot);
                 if (cw != kEmptySlot) {
                     __hip_atomic_store(slot, kEmptySlot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    item = k;
                     return cw;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -1436,12 +1459,13 @@ kaneko_search_kernel(SearchParams p) {
         if (p.in_queue) {  // concurrent with the first pass: take hand-offs as they come
             uint32_t ndone = 0;
             for (;;) {
-                uint32_t cw = 0;
-                if (lane == 0) cw = tail_dequeue(p);
+                uint32_t cw = 0, item = 0;
+                if (lane == 0) cw = tail_dequeue(p, item);
                 cw = (uint32_t)__shfl((int)cw, 0, 64);
+                item = (uint32_t)__shfl((int)item, 0, 64);
                 if (cw == kEmptySlot) break;
                 if (cw >= p.count) continue;  // never a valid slot value
-                search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, 0u);
+                search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item);
                 ++ndone;
             }
             wave_done(p, lane, ndone);
@@ -1459,6 +1483,7 @@ kaneko_search_kernel(SearchParams p) {
     // Work queue left by the fast path: sub-queue x holds items x, x+8, x+16, ...; a wave
     // drains its own XCD's sub-queue first (one L2-local atomic per codeword), then steals.
     const uint32_t total = *p.qcount;
+    const uint32_t nfront = p.qfront_n ? *p.qfront_n : total;  // items past it: the back
     if ((blockIdx.x * kWavesPerBlock + wid) >= total) return;  // more waves than work
     int x = xcc_id();
     uint32_t ndone = 0;
@@ -1472,7 +1497,8 @@ kaneko_search_kernel(SearchParams p) {
             ++exhausted;
             continue;
         }
-        const uint32_t cw = p.queue[item];
+        const uint32_t qi = item < nfront ? item : p.count - 1u - (item - nfront);
+        const uint32_t cw = p.queue[qi];
         if (cw < p.count)  // never otherwise: no access outside the batch
             search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item);
         ++ndone;

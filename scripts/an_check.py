@@ -71,8 +71,12 @@ for (m, t, J, snr, B) in [] if not PARITY else [(6, 6, 15, 5.0, 1 << 16), (6, 6,
 # timing of the headline batch per stage
 for J, snr in [(15, 5.0), (15, 4.0), (15, 6.0), (-1, 5.0)]:
     lims = [int(x) for x in os.environ.get("AN_LIMITS", "8").split(",")]
-    for analytic, limit, conc, hyb in [(False, 4, 0, 0)] + [(True, L, 0, 0) for L in lims]:
-        os.environ["BCHK_TAIL_CONCURRENT"] = str(conc)
+    confs = [(False, 4, 0, 0)] + [(True, L, 0, 0) for L in lims]
+    for blocks in [int(x) for x in os.environ.get("AN_CONC_BLOCKS", "").split(",") if x]:
+        confs.append((True, lims[0], blocks, 0))
+    for analytic, limit, conc, hyb in confs:
+        os.environ["BCHK_TAIL_CONCURRENT"] = str(int(conc > 0))
+        os.environ["BCHK_TAIL_BLOCKS"] = str(conc or 64)
         os.environ["BCHK_TAIL_MIN_BOUND"] = str(hyb)
         d = mk(6, 6, J, analytic, limit)
         _, y, _ = d.generate(snr, 1 << 20, seed=1)
