@@ -224,9 +224,13 @@ typedef struct bchk_polar bchk_polar;
  * (out/external/MixedKernelListDecoder.cpp:9): spec is the text of the reference's code
  * specification (out/external/MixedKernelEncoder.cpp:7-98: "N K d layers #shortened
  * #punctured", kernel names, shortened / punctured symbols, U - K freezing constraints).
- * The GPU decoder takes Arikan ("A") layers, 1 <= list_size <= 32, and lengths whose
- * per-wave state fits the 160 KiB LDS (U <= 1024 at L = 16, 2048 at L = 8). */
+ * Kernels: Arikan ("A") layers, and matrix kernels ("-file" / "<file", a size and size^2
+ * entries, Kernel.cpp:93-107 -- e.g. BCH-derived kernels) of size <= 16, whose kernel LLRs are
+ * the trellis min-sum of out/external/TrellisKernelProcessor.cpp:234-294 (polar_mixed.hip);
+ * 1 <= list_size <= 32, lengths whose per-wave state fits the 160 KiB LDS (U <= 1024 at
+ * L = 16, 2048 at L = 8 for all-Arikan codes). Kernel files are read relative to kdir. */
 int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **out);
+int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, int device, bchk_polar **out);
 void bchk_polar_destroy(bchk_polar *pc);
 /* N (transmitted length), K, U (unshortened length), L */
 int bchk_polar_params(const bchk_polar *pc, int *n, int *k, int *unshortened, int *list_size);

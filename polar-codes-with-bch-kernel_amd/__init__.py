@@ -35,7 +35,7 @@ EXPORTS = (
     "bchk_profile_read", "bchk_profile_read_stages", "bchk_path_counts", "bchk_tail_count",
     "bchk_tail_stats", "bchk_tail_diag_read", "bchk_set_fast_path", "bchk_set_analytic",
     "bchk_set_chunk_limit", "bchk_set_syndrome_table",
-    "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_polar_create",
+    "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_polar_create", "bchk_polar_create_kdir",
     "bchk_polar_destroy", "bchk_polar_params", "bchk_polar_decode_host", "bchk_polar_decode_device",
     "bchk_polar_encode_host", "bchk_polar_sync", "bchk_polar_stream", "bchk_last_error", "bchk_version",
 )
@@ -104,6 +104,7 @@ def lib():
     L.bchk_set_fast_path.argtypes = [vp, i32]
     L.bchk_set_syndrome_table.argtypes = [vp, i32]
     L.bchk_polar_create.argtypes = [C.c_char_p, i32, i32, C.POINTER(vp)]
+    L.bchk_polar_create_kdir.argtypes = [C.c_char_p, C.c_char_p, i32, i32, C.POINTER(vp)]
     L.bchk_polar_destroy.argtypes = [vp]
     L.bchk_polar_destroy.restype = None
     L.bchk_polar_params.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
@@ -338,9 +339,10 @@ class PolarListDecoder:
     :9, :211-268) on the GPU: batched SC-list decoding of a polar code given by the
     reference's specification text (Arikan layers)."""
 
-    def __init__(self, spec, L, device=0):
+    def __init__(self, spec, L, device=0, kernel_dir=None):
         h = C.c_void_p()
-        _check(lib().bchk_polar_create(spec.encode(), L, device, C.byref(h)))
+        _check(lib().bchk_polar_create_kdir(spec.encode(), kernel_dir.encode() if kernel_dir else None, L, device,
+                                            C.byref(h)))
         self._h = h
         n, k, u, l = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         _check(lib().bchk_polar_params(h, C.byref(n), C.byref(k), C.byref(u), C.byref(l)))

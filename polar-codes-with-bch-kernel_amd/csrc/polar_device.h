@@ -25,11 +25,46 @@ struct PolarParams {
 
 constexpr uint16_t kPhaseFrozen = 1u, kPhaseCorr = 0x100u;
 
+
 // (constexpr: usable from device code too.) Per-path strides in LDS, padded by 16 bytes so that the same element of consecutive paths
 // falls in different banks (64 x 4 B banks): S holds U floats, C 3U bytes.
 constexpr int polar_path_s(int U) { return ((U + 3) & ~3) + 4; }
 constexpr int polar_path_c(int U) { return ((3 * U + 15) & ~15) + 16; }
 constexpr int polar_rec_words(int K) { return K > 0 ? (K + 31) / 32 : 1; }
+
+// Mixed kernels (polar_mixed.hip): layer j has a kernel of size ksize[j] (Arikan or a
+// matrix, rows as bitmasks krows[j * kPolarMaxKernel + r], bit c = K[r][c]); outer[λ] =
+// U / (ksize[0] ... ksize[λ-1]); per path S layer λ at soff[λ] (outer[λ] floats, λ >= 1), C
+// layer λ at coff[λ] (outer[λ] ksize[λ-1] bytes, C_0 = U), matrix offset states at ooff[j].
+constexpr int kPolarMaxKernel = 32;
+constexpr int kPolarMaxMatrixGpu = 16;  // coset enumeration 2^(size - 1 - phase) per LLR
+struct PolarMixedParams {
+    const float *llr;
+    uint8_t *info, *cw;
+    float *metric;
+    int32_t *count;
+    const int16_t *symmap;
+    const uint16_t *phase;
+    const uint64_t *dfcorr;
+    const int16_t *cwpos;
+    const uint32_t *krows;  // [nl][kPolarMaxKernel]
+    uint32_t B;
+    int32_t nl, U, N, K, L;
+    int32_t ssize, csize, osize;
+    int32_t ksize[kPolarMaxLayers], outer[kPolarMaxLayers + 1];
+    int32_t soff[kPolarMaxLayers + 1], coff[kPolarMaxLayers + 1], ooff[kPolarMaxLayers];
+    uint8_t arikan[kPolarMaxLayers];
+};
+
+inline uint32_t polar_mixed_lds_bytes(int U, int L, int K, int ssize, int csize, int osize, int nl) {
+    uint32_t b = (4u * (uint32_t)U + 15u) & ~15u;                                     // channel
+    b += 4u * (uint32_t)ssize * (uint32_t)L + (uint32_t)csize * (uint32_t)L;           // S, C
+    b = (b + (uint32_t)osize * (uint32_t)L + 15u) & ~15u;                              // offsets
+    b = (b + 2u * (uint32_t)U + 15u) & ~15u;                                           // phases
+    b += 4u * (uint32_t)kPolarMaxKernel * (uint32_t)nl;                                // rows
+    b += 4u * (uint32_t)L + 4u * (uint32_t)L * (uint32_t)polar_rec_words(K);            // act, rec
+    return (b + 15u) & ~15u;
+}
 
 // LDS bytes of one wave's state (see polar_sclist.hip): channel LLRs, per path S and C,
 // the phase table, the active-path list and per path the information bits decided so far.

@@ -24,6 +24,8 @@ using namespace bchk;
 namespace bchk {
 hipError_t launch_polar(const PolarParams &p, int grid, size_t lds, hipStream_t s);
 const void *polar_kernel_ptr();
+hipError_t launch_polar_mixed(const PolarMixedParams &p, int grid, size_t lds, hipStream_t s);
+const void *polar_mixed_kernel_ptr();
 void set_last_error(const char *msg);  // bchk_host.cpp: the message bchk_last_error returns
 }  // namespace bchk
 
@@ -70,6 +72,14 @@ struct PBuf {
 
 struct bchk_polar {
     int N = 0, K = 0, U = 0, n = 0, L = 0, device = 0;
+    // layers: kernel size, Arikan flag, rows as bitmasks (bit c = K[r][c]); mixed = any
+    // matrix layer (decoded by polar_mixed_kernel)
+    bool mixed = false;
+    std::vector<int> ksize;
+    std::vector<uint8_t> arikan;
+    std::vector<uint32_t> krows;  // [layer][kPolarMaxKernel]
+    PolarMixedParams mp{};        // the mixed layout (sizes, offsets)
+    size_t off_krows = 0;
     std::vector<int16_t> symmap, infopos, cwpos;
     std::vector<uint8_t> frozen;
     std::vector<int8_t> dfbit;
@@ -89,20 +99,78 @@ namespace {
 // The specification (MixedKernelEncoder.cpp:7-98): header, kernel names, shortened and
 // punctured symbols, then U - K freezing constraints "w t_1 ... t_w" (ascending, the frozen
 // symbol last). The GPU decoder takes Arikan layers ("A"); other kernels are rejected.
-int parse_spec(bchk_polar *c, const char *spec) {
+// GetKernelByName (Kernel.cpp:235-252): "A" (any case), or a matrix file "-path" / "<path"
+// (relative to kdir) holding the size and size^2 entries (Kernel.cpp:93-107); the kernel must
+// be invertible (Kernel.cpp:155-176).
+int read_kernel(const std::string &name, const char *kdir, int *size, uint32_t *rows, bool *arikan) {
+    if (name == "A" || name == "a") {
+        *size = 2;
+        rows[0] = 1u;       // 1 0
+        rows[1] = 3u;       // 1 1  (Kernel.cpp:8-12)
+        *arikan = true;
+        return 0;
+    }
+    if (name.empty() || (name[0] != '-' && name[0] != '<')) return pfail(BCHK_EINVAL, "Unknown kernel %s", name.c_str());
+    std::string path = name.substr(1);
+    if (!path.empty() && path[0] != '/' && kdir && kdir[0]) path = std::string(kdir) + "/" + path;
+    FILE *f = fopen(path.c_str(), "r");
+    if (!f) return pfail(BCHK_EINVAL, "Error reading kernel file %s", path.c_str());
+    int l = 0;
+    if (fscanf(f, "%d", &l) != 1 || l < 2 || l > kPolarMaxKernel) {
+        fclose(f);
+        return pfail(BCHK_EINVAL, "Error reading kernel file %s (size)", path.c_str());
+    }
+    for (int r = 0; r < l; ++r) {
+        rows[r] = 0;
+        for (int q = 0; q < l; ++q) {
+            unsigned v;
+            if (fscanf(f, "%u", &v) != 1) {
+                fclose(f);
+                return pfail(BCHK_EINVAL, "Error parsing kernel file %s", path.c_str());
+            }
+            if (v) rows[r] |= 1u << q;
+        }
+    }
+    fclose(f);
+    std::vector<uint32_t> a(rows, rows + l);  // GF(2) rank
+    for (int col = 0, r0 = 0; col < l; ++col) {
+        int piv = r0;
+        while (piv < l && !((a[piv] >> col) & 1u)) ++piv;
+        if (piv == l) return pfail(BCHK_EINVAL, "Kernel is singular (%s)", path.c_str());
+        std::swap(a[piv], a[r0]);
+        for (int r = 0; r < l; ++r)
+            if (r != r0 && ((a[r] >> col) & 1u)) a[r] ^= a[r0];
+        ++r0;
+    }
+    if (l > kPolarMaxMatrixGpu)
+        return pfail(BCHK_EINVAL, "matrix kernel of size %d: the GPU SC-list decoder takes sizes up to %d", l,
+                     kPolarMaxMatrixGpu);
+    *size = l;
+    *arikan = false;
+    return 0;
+}
+
+int parse_spec(bchk_polar *c, const char *spec, const char *kdir) {
     std::istringstream in(spec);
     int N, K, dmin, layers, nsh, npu;
     if (!(in >> N >> K >> dmin >> layers >> nsh >> npu)) return pfail(BCHK_EINVAL, "Error reading file header");
     if (K > N || K < 0 || N <= 0) return pfail(BCHK_EINVAL, "Code dimension cannot exceed code length");
     if (layers < 1 || layers > kPolarMaxLayers) return pfail(BCHK_EINVAL, "%d layers unsupported", layers);
+    c->ksize.assign(layers, 2);
+    c->arikan.assign(layers, 1);
+    c->krows.assign((size_t)layers * kPolarMaxKernel, 0u);
+    long Ul = 1;
     for (int i = 0; i < layers; ++i) {
         std::string name;
         if (!(in >> name)) return pfail(BCHK_EINVAL, "missing kernel name %d", i);
-        if (!(name == "A" || name == "a"))
-            return pfail(BCHK_EINVAL, "kernel %s: the GPU SC-list decoder takes Arikan (A) layers only",
-                         name.c_str());
+        bool ar = false;
+        if (int rc = read_kernel(name, kdir, &c->ksize[i], &c->krows[(size_t)i * kPolarMaxKernel], &ar)) return rc;
+        c->arikan[i] = ar ? 1 : 0;
+        c->mixed = c->mixed || !ar;
+        Ul *= c->ksize[i];
+        if (Ul > 16384) return pfail(BCHK_EINVAL, "length %ld exceeds 16384", Ul);
     }
-    const int U = 1 << layers;
+    const int U = (int)Ul;
     if (N + nsh + npu != U) return pfail(BCHK_EINVAL, "Code length mismatch");
     c->N = N;
     c->K = K;
@@ -167,6 +235,10 @@ int parse_spec(bchk_polar *c, const char *spec) {
 extern "C" {
 
 int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **out) {
+    return bchk_polar_create_kdir(spec, nullptr, list_size, device, out);
+}
+
+int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, int device, bchk_polar **out) {
     if (!out || !spec) return pfail(BCHK_EINVAL, "NULL argument");
     *out = nullptr;
     if (list_size < 1 || list_size > kPolarMaxList)
@@ -175,11 +247,32 @@ int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **
     bchk_polar *c = new bchk_polar();
     c->L = list_size;
     c->device = device;
-    if (int rc = parse_spec(c, spec)) {
+    if (int rc = parse_spec(c, spec, kdir)) {
         delete c;
         return rc;
     }
-    c->lds = polar_lds_bytes(c->U, c->L, c->K);
+    if (c->mixed) {  // the mixed layout (oracle/polar_oracle.c plr_decode's offsets)
+        PolarMixedParams &m = c->mp;
+        const int nl = c->n;
+        m.nl = nl;
+        m.outer[0] = c->U;
+        for (int j = 0; j < nl; ++j) {
+            m.ksize[j] = c->ksize[j];
+            m.arikan[j] = c->arikan[j];
+            m.outer[j + 1] = m.outer[j] / c->ksize[j];
+        }
+        int so = 0, co = 0, oo = 0;
+        for (int lam = 1; lam <= nl; ++lam) { m.soff[lam] = so; so += m.outer[lam]; }
+        for (int lam = 0; lam <= nl; ++lam) { m.coff[lam] = co; co += lam ? m.outer[lam] * c->ksize[lam - 1] : m.outer[0]; }
+        for (int j = 0; j < nl; ++j) { m.ooff[j] = oo; if (!c->arikan[j]) oo += c->ksize[j] * m.outer[j + 1]; }
+        m.soff[0] = 0;
+        m.ssize = (so + 3) & ~3;
+        m.csize = (co + 15) & ~15;
+        m.osize = (oo + 15) & ~15;
+        c->lds = polar_mixed_lds_bytes(c->U, c->L, c->K, m.ssize, m.csize, m.osize, nl);
+    } else {
+        c->lds = polar_lds_bytes(c->U, c->L, c->K);
+    }
     if (c->lds > 160 * 1024) {
         const size_t need = c->lds;
         const int U = c->U;
@@ -211,6 +304,7 @@ int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **
     c->off_phase = o; o = al(o + 2 * (size_t)c->U);
     c->off_cwpos = o; o = al(o + 2 * (size_t)c->N);
     c->off_dfcorr = o; o = al(o + 8 * (size_t)c->U);
+    c->off_krows = o; o = al(o + 4 * c->krows.size());
     std::vector<uint8_t> blob(o, 0);
     memcpy(blob.data() + c->off_symmap, c->symmap.data(), 2 * (size_t)c->U);
     {
@@ -221,13 +315,14 @@ int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **
     }
     memcpy(blob.data() + c->off_cwpos, c->cwpos.data(), 2 * (size_t)c->N);
     memcpy(blob.data() + c->off_dfcorr, c->dfcorr.data(), 8 * (size_t)c->U);
+    memcpy(blob.data() + c->off_krows, c->krows.data(), 4 * c->krows.size());
     if (hipMalloc(&c->d_tab, o) != hipSuccess ||
         hipMemcpy(c->d_tab, blob.data(), o, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         bchk_polar_destroy(c);
         return pfail(BCHK_EHIP, "device setup failed");
     }
-    const void *fn = polar_kernel_ptr();
+    const void *fn = c->mixed ? polar_mixed_kernel_ptr() : polar_kernel_ptr();
     if (c->lds > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, c->lds) != hipSuccess || per_cu <= 0) {
@@ -286,6 +381,26 @@ int bchk_polar_decode_device(bchk_polar *c, const float *d_llr, size_t B, uint8_
     p.K = c->K;
     p.L = c->L;
     const int grid = (int)std::min<size_t>((size_t)c->grid, B);
+    if (c->mixed) {
+        PolarMixedParams m = c->mp;
+        m.llr = p.llr;
+        m.info = p.info;
+        m.cw = p.cw;
+        m.metric = p.metric;
+        m.count = p.count;
+        m.symmap = p.symmap;
+        m.phase = p.phase;
+        m.dfcorr = p.dfcorr;
+        m.cwpos = p.cwpos;
+        m.krows = reinterpret_cast<const uint32_t *>(c->d_tab + c->off_krows);
+        m.B = p.B;
+        m.U = c->U;
+        m.N = c->N;
+        m.K = c->K;
+        m.L = c->L;
+        PHIP_TRY(launch_polar_mixed(m, grid, c->lds, stream ? (hipStream_t)stream : c->stream));
+        return 0;
+    }
     PHIP_TRY(launch_polar(p, grid, c->lds, stream ? (hipStream_t)stream : c->stream));
     return 0;
 }
@@ -338,9 +453,22 @@ int bchk_polar_encode_host(const bchk_polar *c, const uint8_t *info, size_t B, u
                 u[i] = in[k++] & 1;
             }
         }
-        for (int st = 1; st < c->U; st <<= 1)
-            for (int i = 0; i < c->U; ++i)
-                if (!(i & st)) u[i] ^= u[i + st];
+        // the transform, innermost layer first (MixedKernelEncoder.cpp:159-170): each block of
+        // `next` symbols, viewed as l rows of `stride`, becomes (rows) x K
+        std::vector<uint8_t> t(c->U);
+        for (int L = c->n - 1, stride = 1; L >= 0; --L) {
+            const int l = c->ksize[L], next = stride * l;
+            const uint32_t *kr = &c->krows[(size_t)L * kPolarMaxKernel];
+            for (int b0 = 0; b0 < c->U; b0 += next)
+                for (int i = 0; i < l; ++i)
+                    for (int s2 = 0; s2 < stride; ++s2) {
+                        uint8_t acc = 0;
+                        for (int j = 0; j < l; ++j) acc ^= (uint8_t)(u[b0 + j * stride + s2] & ((kr[j] >> i) & 1u));
+                        t[b0 + i * stride + s2] = acc;
+                    }
+            u.swap(t);
+            stride = next;
+        }
         for (int i = 0; i < c->N; ++i) cw[b * c->N + i] = u[c->cwpos[i]];
     }
     return 0;

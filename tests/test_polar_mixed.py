@@ -1,0 +1,139 @@
+"""SC-list decoding over MIXED kernels on the GPU (csrc/polar_mixed.hip): Arikan layers and
+matrix kernels (the reference's kernel files, Kernel.cpp:93-107 -- e.g. BCH-derived kernels),
+whose kernel LLRs are the trellis min-sum of out/external/TrellisKernelProcessor.cpp:234-294.
+Bit for bit against the C restatement (oracle/polar_oracle.c; its parity is unpinned, as
+for the Arikan decoder -- SURVEY.md §8c): list counts, information vectors, codewords, f32
+path metrics."""
+import os
+
+import numpy as np
+import pytest
+
+from bchk_pkg import load
+from polar_lib import PolarOracle, awgn_llr
+
+
+def _kernel_text(K):
+    return f"{len(K)}\n" + "\n".join(" ".join(str(int(v)) for v in row) for row in K) + "\n"
+
+
+def _lower_kernel(l, seed):
+    """An invertible l x l kernel: unit lower-triangular with random entries below, rows
+    then permuted among equal-weight classes so it is not a Kronecker power."""
+    rng = np.random.default_rng(seed)
+    K = np.tril(rng.integers(0, 2, (l, l)), -1).astype(np.uint8)
+    np.fill_diagonal(K, 1)
+    K[-1, :] = 1  # the all-ones row last, as polarising kernels have
+    return K
+
+
+KERNELS = {
+    "k4": np.array([[1, 0, 0, 0], [1, 0, 1, 0], [1, 1, 0, 0], [1, 1, 1, 1]], np.uint8),
+    "a2": np.array([[1, 0], [1, 1]], np.uint8),
+    "k8": _lower_kernel(8, 3),
+    "k16": _lower_kernel(16, 5),
+    "k3": np.array([[1, 0, 0], [1, 1, 0], [1, 0, 1]], np.uint8),
+}
+
+
+@pytest.fixture(scope="module")
+def kdir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("kernels")
+    for name, K in KERNELS.items():
+        (d / f"{name}.txt").write_text(_kernel_text(K))
+    return str(d)
+
+
+def mixed_spec(layers, K, dyn=0, punct=(), seed=0):
+    """Spec text over the given layer names ("A" or a kernel file name): the U - K lowest
+    indices frozen except a few swapped for variety, `dyn` of them dynamically frozen."""
+    sizes = [2 if name == "A" else len(KERNELS[name]) for name in layers]
+    U = int(np.prod(sizes))
+    rng = np.random.default_rng(seed)
+    order = list(range(U))
+    for _ in range(U // 8):  # a few swaps near the boundary
+        i = int(rng.integers(max(0, U - K - 4), min(U, U - K + 4)))
+        j = int(rng.integers(max(0, U - K - 4), min(U, U - K + 4)))
+        order[i], order[j] = order[j], order[i]
+    frozen = sorted(order[:U - K])
+    dynset = set(rng.choice([f for f in frozen if f >= 2], size=min(dyn, len([f for f in frozen if f >= 2])),
+                            replace=False).tolist()) if dyn else set()
+    names = ["A" if n == "A" else f"-{n}.txt" for n in layers]
+    lines = [f"{U - len(punct)} {K} 0 {len(layers)} 0 {len(punct)}", " ".join(names)]
+    if punct:
+        lines.append(" ".join(str(p) for p in punct))
+    for f in frozen:
+        if f in dynset:
+            a, b = sorted(rng.choice(f, size=2, replace=False).tolist())
+            lines.append(f"3 {a} {b} {f}")
+        else:
+            lines.append(f"1 {f}")
+    return "\n".join(lines) + "\n"
+
+
+def _same(got, want):
+    gc, gi, gw, gm = got
+    wc, wi, ww, wm = want
+    np.testing.assert_array_equal(gc, wc)
+    for b in range(len(wc)):
+        c = wc[b]
+        np.testing.assert_array_equal(gi[b, :c], wi[b, :c], err_msg=f"info, codeword {b}")
+        np.testing.assert_array_equal(gw[b, :c], ww[b, :c], err_msg=f"codeword, row {b}")
+        np.testing.assert_array_equal(gm[b, :c].view(np.uint32), wm[b, :c].view(np.uint32),
+                                      err_msg=f"metrics, row {b}")
+
+
+def test_spec_errors_before_the_device(kdir, tmp_path):
+    # matrix kernels are parsed and checked on the host, with or without a GPU
+    F = load()
+    (tmp_path / "sing.txt").write_text("3\n1 0 0\n1 0 0\n0 1 1\n")
+    (tmp_path / "big.txt").write_text(_kernel_text(_lower_kernel(20, 1)))
+    for name, msg in [("sing", "singular"), ("big", "sizes up to 16"), ("missing", "Error reading kernel file")]:
+        spec = f"20 10 0 1 0 0\n-{name}.txt\n" + "".join(f"1 {i}\n" for i in range(10))
+        with pytest.raises(F.BchkError, match=msg):
+            F.PolarListDecoder(spec, 4, kernel_dir=str(tmp_path))
+    with pytest.raises(F.BchkError, match="Unknown kernel"):
+        F.PolarListDecoder("4 2 0 1 0 0\nB\n1 0\n1 1\n", 4)
+
+
+CODES = [
+    (("k4", "A"), 4, 0, ()),            # the oracle test's matrix4 code, N = 8
+    (("k8", "A", "A"), 16, 2, ()),      # U = 32
+    (("A", "k8", "A"), 14, 3, (5, 9)),  # punctured
+    (("k16", "A"), 16, 2, ()),          # a 16 x 16 matrix kernel, U = 32
+    (("A", "A", "k16"), 32, 4, ()),     # U = 64, the matrix layer innermost
+    (("k3", "k4", "A"), 12, 2, ()),     # odd kernel size, U = 24
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layers,K,dyn,punct", CODES, ids=["-".join(c[0]) for c in CODES])
+@pytest.mark.parametrize("L", [1, 2, 4, 8, 16])
+def test_gpu_mixed_matches_oracle(kdir, layers, K, dyn, punct, L):
+    spec = mixed_spec(layers, K, dyn, punct, seed=len(layers) * 11 + K)
+    o = PolarOracle(spec, kdir)
+    d = load().PolarListDecoder(spec, L, kernel_dir=kdir)
+    assert (d.N, d.K, d.U) == (o.N, o.K, o.U)
+    rng = np.random.default_rng(L + K)
+    info = rng.integers(0, 2, (40, K)).astype(np.uint8)
+    cw = o.encode(info)
+    np.testing.assert_array_equal(d.encode(info), cw)  # the host encoder over mixed layers
+    for snr in (0.0, 2.0):
+        llr = awgn_llr(cw, snr, K / o.N, seed=int(snr * 10) + L)
+        _same(d.decode(llr), o.decode_batch(llr, L))
+
+
+@pytest.mark.gpu
+def test_matrix_arikan_kernel_equals_the_arikan_decoder(kdir):
+    # 2x2 matrix kernels equal to Arikan's through the mixed decoder give the Arikan decoder's
+    # (polar_sclist.hip) lists exactly
+    from polar_lib import arikan_spec
+    base = arikan_spec(6, 28, dyn=4, seed=4)
+    head, kern, rest = base.split("\n", 2)
+    mixed = head + "\n" + " ".join(["-a2.txt"] * 6) + "\n" + rest
+    F = load()
+    da, dm = F.PolarListDecoder(base, 8), F.PolarListDecoder(mixed, 8, kernel_dir=kdir)
+    o = PolarOracle(base)
+    info = np.random.default_rng(1).integers(0, 2, (64, 28)).astype(np.uint8)
+    llr = awgn_llr(o.encode(info), 1.5, 28 / 64, seed=8)
+    _same(dm.decode(llr), da.decode(llr))

@@ -59,7 +59,7 @@ def test_create_fails_loudly_without_gpu():
     (arikan_spec(5, 16), 33, "list size"),
     (arikan_spec(11, 1024), 32, "LDS"),
     ("10 5 0 3 0 0\nA A A\n1 0\n1 1\n1 2\n", 4, "mismatch|length"),
-    ("8 4 0 2 0 0\n-k4.txt A\n1 0\n1 1\n1 2\n1 4\n", 4, "Arikan"),
+    ("8 4 0 2 0 0\n-k4.txt A\n1 0\n1 1\n1 2\n1 4\n", 4, "Error reading kernel file"),
     ("garbage", 4, "header"),
 ])
 def test_bad_codes_are_rejected_before_touching_the_device(spec, L, msg):
