@@ -239,9 +239,10 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
     total_words = world * B * args.steps
     value = total_words / elapsed
     # Algorithmic bytes per codeword: 8n B of f64 samples in, n B decoded bits and 8 B l0
-    # out. The fast kernel moves them for all B codewords; the exact, tail
-    # and cooperative kernels re-read/write them for the codewords handed to them.
-    bytes_per_cw = 9 * n + 8
+    # out, + n B of sent word read by the fused counters (the default step).
+    # The fast kernel moves them for all B codewords; the exact, tail and cooperative
+    # kernels re-read/write them for the codewords handed to them.
+    bytes_per_cw = 9 * n + 8 + (0 if args.unfused else n)
     launches = max(1, launches)
     tm = dec_tmax(args.t)
     # the lane-per-codeword fast kernel exists for n <= 63 and small t (csrc/bchk_fast.hip
