@@ -27,7 +27,70 @@ def _lower_kernel(l, seed):
     return K
 
 
+def _bch_kernel(power, prim):
+    """The reference's nested extended-BCH kernel (root bchCoder.cpp:356-389 makeMatrix):
+    column 0 all ones, row 1 = x^0 shifted, row deg(g) of each growing generator
+    g = lcm(M_2, ..., M_i) holds g (from column 1), the rows between hold shifts of the previous
+    generator; GF(2^power) from the primitive polynomial `prim`."""
+    n = (1 << power) - 1
+    el, x = [], 1
+    for _ in range(n):
+        el.append(x)
+        x <<= 1
+        if x >> power:
+            x ^= prim
+    log = {v: k for k, v in enumerate(el)}
+
+    def minpoly(i):
+        coset, j = [], i % n
+        while j not in coset:
+            coset.append(j)
+            j = 2 * j % n
+        poly = [1]
+        for j in coset:  # multiply by (x + alpha^j)
+            q = [0] * (len(poly) + 1)
+            for k, c in enumerate(poly):
+                if c:
+                    q[k] ^= el[(log[c] + j) % n]
+                q[k + 1] ^= c
+            poly = q
+        return [int(c) for c in poly]
+
+    def mul(a, b):
+        r = [0] * (len(a) + len(b) - 1)
+        for i, u in enumerate(a):
+            for j, v in enumerate(b):
+                r[i + j] ^= u & v
+        return r
+
+    def divides(a, b):  # b | a over GF(2)
+        a = list(a)
+        while len(a) >= len(b):
+            if a[-1]:
+                for k, c in enumerate(b):
+                    a[len(a) - len(b) + k] ^= c
+            a.pop()
+        return not any(a)
+
+    M = np.zeros((n + 1, n + 1), np.uint8)
+    M[:, 0] = 1
+    M[1, 1] = 1
+    g, gold = [1], 1
+    for i in range(2, (n - 1) // 2 + 1 if power != 2 else 3):
+        poly = minpoly(i)
+        if gold >= len(poly) and divides(g, poly):
+            continue
+        gnew = len(poly) + gold - 1
+        M[gnew, 1:1 + gnew] = mul(poly, g)
+        for cnt, j in enumerate(range(gold, gnew - 1), start=1):
+            M[j + 1, cnt + 1:cnt + 1 + gold] = g[:gold]
+        g, gold = list(M[gnew, 1:gnew + 1]), gnew
+    return M
+
+
 KERNELS = {
+    "bch8": _bch_kernel(3, 0b1011),
+    "bch16": _bch_kernel(4, 0b10011),
     "k4": np.array([[1, 0, 0, 0], [1, 0, 1, 0], [1, 1, 0, 0], [1, 1, 1, 1]], np.uint8),
     "a2": np.array([[1, 0], [1, 1]], np.uint8),
     "k8": _lower_kernel(8, 3),
@@ -103,7 +166,20 @@ CODES = [
     (("k16", "A"), 16, 2, ()),          # a 16 x 16 matrix kernel, U = 32
     (("A", "A", "k16"), 32, 4, ()),     # U = 64, the matrix layer innermost
     (("k3", "k4", "A"), 12, 2, ()),     # odd kernel size, U = 24
+    (("bch16", "A"), 16, 2, ()),        # the reference's 16 x 16 extended-BCH kernel
+    (("A", "bch8", "A"), 16, 2, (3,)),  # its 8 x 8 one, between Arikan layers
+    (("bch16", "bch8"), 64, 4, ()),     # two BCH kernels, U = 128
 ]
+
+
+def test_bch_kernels_are_the_nested_construction():
+    # row weights / triangular shape of root bchCoder.cpp's makeMatrix output, and invertible
+    for name in ("bch8", "bch16"):
+        M = KERNELS[name].astype(np.int64)
+        l = len(M)
+        assert (M[:, 0] == 1).all() and M[-1].sum() == l
+        assert all(M[r, r] == 1 and not M[r, r + 1:].any() for r in range(l))  # lower triangular
+        assert abs(round(np.linalg.det(M))) % 2 == 1
 
 
 @pytest.mark.gpu
