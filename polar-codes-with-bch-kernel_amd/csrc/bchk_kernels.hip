@@ -1672,6 +1672,18 @@ kaneko_coop_kernel(SearchParams p) {
     constexpr int kAcceptor = 0;  // the oldest wave: the SIMD arbiter favours it
     constexpr int kCoopSlots = coop_slots<NW>();
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    {   // nothing handed off and every producer finished (the usual case at high SNR): the
+        // block leaves before staging the tables
+        __shared__ uint32_t idle;
+        if (threadIdx.x == 0) {
+            const uint32_t total = p.exact_total ? *p.exact_total : p.count;
+            const bool fin = exact_finished(p) >= total;
+            mem_drain();
+            idle = fin && ld_rlx(p.heavy_tail) == 0u && ld_rlx(p.heavy_tail2) == 0u ? 1u : 0u;
+        }
+        __syncthreads();
+        if (idle) return;
+    }
     load_tables(smem, p.tables, p.td.bytes);
     const uint8_t *ex = smem + p.td.off_exp;
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);

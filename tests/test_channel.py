@@ -33,6 +33,7 @@ def test_channel_words_are_codewords_with_gaussian_noise(m, t, snr):
     g = np.array(d.g, np.uint8)
     dtx = torch.zeros((B, n), dtype=torch.uint8, device="cuda")
     dy = torch.zeros((B, n), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # torch's fills run on its own stream, the decoder's on another
     d.generate_device(snr, B, dtx.data_ptr(), dy.data_ptr(), seed=5, word0=123)
     d.sync()
     tx, y = dtx.cpu().numpy(), dy.cpu().numpy()
@@ -50,6 +51,7 @@ def test_channel_words_are_codewords_with_gaussian_noise(m, t, snr):
     # a word depends only on (seed, word index): sub-ranges reproduce the whole
     dtx2 = torch.zeros((B, n), dtype=torch.uint8, device="cuda")
     dy2 = torch.zeros((B, n), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
     h = 7777
     d.generate_device(snr, h, dtx2.data_ptr(), dy2.data_ptr(), seed=5, word0=123)
     d.generate_device(snr, B - h, dtx2[h:].data_ptr(), dy2[h:].data_ptr(), seed=5, word0=123 + h)

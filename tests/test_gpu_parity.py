@@ -409,6 +409,7 @@ def test_fused_counters_equal_decode_then_count(m, t, J, snr, exec_path):
         dst = torch.zeros((B, 56), dtype=torch.uint8, device="cuda")
         c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
         c6[:] = torch.tensor([3, 5, 7, 11, 13, 17])  # the calls add to what is there
+        torch.cuda.synchronize()  # torch's copies / fills run on its stream, not the decoder's
         if fused:
             d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), 0,
                                   c6.data_ptr())
@@ -429,6 +430,7 @@ def test_fused_counters_equal_decode_then_count(m, t, J, snr, exec_path):
     # a second fused call adds the same counts again (the partial slots were zeroed)
     dres = torch.from_numpy(fill.copy()).cuda()
     c6 = torch.from_numpy(c1.copy()).cuda()
+    torch.cuda.synchronize()
     d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), 0, 0, c6.data_ptr())
     d.sync()
     np.testing.assert_array_equal(c6.cpu().numpy(), 2 * c1 - np.array([3, 5, 7, 11, 13, 17]))
@@ -465,6 +467,7 @@ def test_sub_batch_pipelines_match_one_pipeline(m, t, J, snr):
     for d in (one, multi):
         dres = torch.zeros((B, d.n), dtype=torch.uint8, device="cuda")
         c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
         d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), 0, 0, c6.data_ptr())
         d.sync()
         outs.append((dres.cpu().numpy(), c6.cpu().numpy()))
