@@ -249,6 +249,40 @@ int bchk_polar_encode_host(const bchk_polar *pc, const uint8_t *info, size_t B, 
 int bchk_polar_sync(bchk_polar *pc);
 void *bchk_polar_stream(bchk_polar *pc);
 
+/* ---- BCH polar-kernel construction and the column-permutation search (root bchCoder.cpp;
+ * csrc/kernel_search.hip). Kernels are row-major l x l bytes (0/1). */
+/* makeMatrix (root bchCoder.cpp:356-389): the nested extended-BCH kernel of size 2^power
+ * (2 <= power <= 5), GF(2^power) from the reference's primitive polynomials
+ * (src/main.cpp:14-15). Columns in power order: column 0 the extension, column p + 1 the
+ * position of alpha^p. */
+int bchk_kernel_ebch(int power, uint8_t *K);
+/* swapColumns' reordering (root bchCoder.cpp:478-496): columns 0..2 kept, column i >= 3
+ * takes the column of the field element i. */
+int bchk_kernel_field_order(int power, const uint8_t *K, uint8_t *out);
+/* The operation counts (SumCount, CmpCount; headers/external/misc.h:84-93) a
+ * CTrellisKernelProcessor (out/external/TrellisKernelProcessor.cpp:69-294) spends on
+ * GetLLRs(1, phase, zero known inputs, llr) for every phase 0..l-1 of the invertible kernel
+ * K (2 <= l <= 32), the score the column search minimises (root bchCoder.cpp:505-515). */
+int bchk_kernel_trellis_cost(const uint8_t *K, int l, const float *llr, int device, uint64_t *sum,
+                             uint64_t *cmp);
+/* The same score for every column map j -> B j with B = L.U (randomInvertibleMatrix, root
+ * bchCoder.cpp:766-785) of a 2^power kernel: sum / cmp hold 2^(power (power - 1)) entries,
+ * indexed by the candidate code whose bit d is the d-th bit randomInvertibleMatrix draws
+ * (row i: l[i][0..i-1], then u[i][i+1..power-1]). */
+int bchk_kernel_column_costs(int power, const uint8_t *K, const float *llr, int device, uint64_t *sum,
+                             uint64_t *cmp);
+#define BCHK_KSEARCH_EXHAUSTIVE 0 /* every L.U product, in code order                    */
+#define BCHK_KSEARCH_RANDOM 1     /* randomSwapColumns: `count` random L.U products drawn  */
+                                  /* from the reference's engine (state *rng_state, in/out) */
+/* randomSwapColumns (root bchCoder.cpp:541-699): the candidate accepted last under the
+ * reference's rule (both counts strictly below the best so far, :651-657), its permuted
+ * kernel best[k][j] = K[k][perm[j]] (:627-629; best / perm may be NULL), its counts and its
+ * index in the candidate sequence (-1: none). Scores come from the GPU (one launch over all
+ * candidates), the acceptance is replayed on the host in candidate order. */
+int bchk_kernel_column_search(int power, const uint8_t *K, const float *llr, int mode, uint64_t count,
+                              uint64_t *rng_state, int device, uint8_t *best, uint32_t *perm,
+                              uint64_t *best_sum, uint64_t *best_cmp, int64_t *best_index);
+
 const char *bchk_last_error(void);
 const char *bchk_version(void);
 

@@ -37,7 +37,9 @@ EXPORTS = (
     "bchk_set_chunk_limit", "bchk_set_syndrome_table",
     "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_polar_create", "bchk_polar_create_kdir",
     "bchk_polar_destroy", "bchk_polar_params", "bchk_polar_decode_host", "bchk_polar_decode_device",
-    "bchk_polar_encode_host", "bchk_polar_sync", "bchk_polar_stream", "bchk_last_error", "bchk_version",
+    "bchk_polar_encode_host", "bchk_polar_sync", "bchk_polar_stream",
+    "bchk_kernel_ebch", "bchk_kernel_field_order", "bchk_kernel_trellis_cost", "bchk_kernel_column_costs",
+    "bchk_kernel_column_search", "bchk_last_error", "bchk_version",
 )
 
 STATS_DTYPE = np.dtype([("decodes", "<u8"), ("comparisons", "<u8"), ("sums", "<u8"),
@@ -124,6 +126,12 @@ def lib():
     L.bchk_profile_read_stages.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
     L.bchk_set_analytic.argtypes = [vp, i32]
     L.bchk_set_chunk_limit.argtypes = [vp, C.c_uint32]
+    L.bchk_kernel_ebch.argtypes = [i32, vp]
+    L.bchk_kernel_field_order.argtypes = [i32, vp, vp]
+    L.bchk_kernel_trellis_cost.argtypes = [vp, i32, vp, i32, C.POINTER(u64), C.POINTER(u64)]
+    L.bchk_kernel_column_costs.argtypes = [i32, vp, vp, i32, vp, vp]
+    L.bchk_kernel_column_search.argtypes = [i32, vp, vp, i32, u64, C.POINTER(u64), i32, vp, vp,
+                                            C.POINTER(u64), C.POINTER(u64), C.POINTER(C.c_int64)]
     L.bchk_last_error.restype = C.c_char_p
     L.bchk_version.restype = C.c_char_p
     _lib = L
@@ -416,6 +424,60 @@ def syndrome_table_info(m, t):
     k, b, p = C.c_uint64(), C.c_uint64(), C.c_uint32()
     _check(lib().bchk_syndrome_table_info(m, t, C.byref(k), C.byref(b), C.byref(p)))
     return k.value, b.value, p.value
+
+
+def kernel_ebch(power):
+    """makeMatrix (root bchCoder.cpp:356-389): the nested extended-BCH kernel, 2^power square."""
+    n = 1 << power
+    K = np.zeros((n, n), np.uint8)
+    _check(lib().bchk_kernel_ebch(power, _p(K)))
+    return K
+
+
+def kernel_field_order(power, K):
+    """swapColumns' column reordering (root bchCoder.cpp:478-496)."""
+    K = np.ascontiguousarray(K, np.uint8)
+    out = np.zeros_like(K)
+    _check(lib().bchk_kernel_field_order(power, _p(K), _p(out)))
+    return out
+
+
+def kernel_trellis_cost(K, llr, device=0):
+    """(SumCount, CmpCount) of CTrellisKernelProcessor::GetLLRs over every phase with zero known
+    inputs (the column search's score), computed on the GPU."""
+    K = np.ascontiguousarray(K, np.uint8)
+    y = np.ascontiguousarray(llr, np.float32)
+    s, c = C.c_uint64(), C.c_uint64()
+    _check(lib().bchk_kernel_trellis_cost(_p(K), K.shape[0], _p(y), device, C.byref(s), C.byref(c)))
+    return s.value, c.value
+
+
+def kernel_column_costs(power, K, llr, device=0):
+    """Scores of every L.U column map (indexed by candidate code), from one GPU launch."""
+    K = np.ascontiguousarray(K, np.uint8)
+    y = np.ascontiguousarray(llr, np.float32)
+    n = 1 << (power * (power - 1))
+    s = np.zeros(n, np.uint64)
+    c = np.zeros(n, np.uint64)
+    _check(lib().bchk_kernel_column_costs(power, _p(K), _p(y), device, _p(s), _p(c)))
+    return s, c
+
+
+KSEARCH_EXHAUSTIVE, KSEARCH_RANDOM = 0, 1
+
+
+def kernel_column_search(power, K, llr, mode=KSEARCH_EXHAUSTIVE, count=0, rng_state=1, device=0):
+    """randomSwapColumns (root bchCoder.cpp:541-699) -> dict(best, perm, sum, cmp, index,
+    rng_state)."""
+    K = np.ascontiguousarray(K, np.uint8)
+    y = np.ascontiguousarray(llr, np.float32)
+    n = 1 << power
+    best = np.zeros((n, n), np.uint8)
+    perm = np.zeros(n, np.uint32)
+    st, s, c, i = C.c_uint64(rng_state), C.c_uint64(), C.c_uint64(), C.c_int64()
+    _check(lib().bchk_kernel_column_search(power, _p(K), _p(y), mode, count, C.byref(st), device,
+                                           _p(best), _p(perm), C.byref(s), C.byref(c), C.byref(i)))
+    return dict(best=best, perm=perm, sum=s.value, cmp=c.value, index=i.value, rng_state=st.value)
 
 
 def version():
