@@ -328,8 +328,117 @@ static void arikan_llr(int phase, int d, const uint8_t *known, const float *src,
     }
 }
 
+/* The trellis itself, for cosets too large to enumerate: CTrellisKernelProcessor's
+ * construction (TrellisKernelProcessor.cpp:69-179, MinimumSpan :7-67) and walk (:260-292)
+ * state by state, float metrics. Same value as the enumeration (min commutes with the
+ * monotone float add along each word's left-to-right sum). */
+static float trellis_minsum_llr(const plr_kernel *k, int phase, const float *y) {
+    const unsigned l = (unsigned)k->size, N = l + 1, K = l - (unsigned)phase;
+    uint64_t M[PLR_MAXKERNEL] = {0};
+    for (unsigned i = 0; i < K; ++i) {
+        M[i] = 0;
+        for (unsigned j = 0; j < l; ++j)
+            if (k->K[(phase + i) * l + j]) M[i] |= 1ull << j;
+    }
+    M[0] |= 1ull << l;
+    unsigned start[PLR_MAXKERNEL + 1], end[PLR_MAXKERNEL + 1], C = 0;
+    for (unsigned c = 0; c < N; ++c) start[c] = end[c] = ~0u;
+    for (unsigned i = 0; i < K; ++i) {
+        int found = 0;
+        for (; C < N; ++C) {
+            if (!((M[i] >> C) & 1)) {
+                for (unsigned j = i + 1; j < K; ++j)
+                    if ((M[j] >> C) & 1) {
+                        M[i] ^= M[j];
+                        found = 1;
+                        break;
+                    }
+                if (found) {
+                    start[C] = i;
+                    break;
+                }
+            } else {
+                start[C] = i;
+                found = 1;
+                break;
+            }
+        }
+        for (unsigned j = i + 1; j < K; ++j)
+            if ((M[j] >> C) & 1) M[j] ^= M[i];
+    }
+    for (int i = (int)K - 1; i >= 0; --i)
+        for (int j = (int)N - 1; j >= 0; --j)
+            if ((M[i] >> j) & 1) {
+                end[j] = (unsigned)i;
+                for (int s = 0; s < i; ++s)
+                    if ((M[s] >> j) & 1) M[s] ^= M[i];
+                break;
+            }
+    unsigned most = 0;
+    for (unsigned j = 0, a = 0; j < l; ++j) { /* states of the widest depth, edges included */
+        if (a + 1 > most) most = a + 1;
+        a += (start[j] != ~0u) - (end[j] != ~0u);
+    }
+    const size_t cap = (size_t)1 << (most + 1);
+    uint64_t *cw0 = calloc(cap, 8), *cw1 = calloc(cap, 8);
+    float *m0 = malloc(cap * 4), *m1 = malloc(cap * 4);
+    unsigned active[PLR_MAXKERNEL + 1], na = 0;
+    m0[0] = 0.0f;
+    for (unsigned j = 0; j < l; ++j) {
+        unsigned B = na;
+        for (unsigned q = 0; q < na; ++q)
+            if (active[q] == end[j]) { B = q; break; }
+        const uint64_t emask = (end[j] == ~0u) ? ~0ull : ((1ull << B) - 1);
+        const uint64_t ns = 1ull << na;
+        const unsigned na1 = na + (start[j] != ~0u) - (end[j] != ~0u);
+        for (uint64_t S = 0; S < (1ull << na1); ++S) m1[S] = INFINITY;
+        const float Y = y[j], aY = fabsf(Y);
+        const unsigned HD = Y < 0;
+        for (uint64_t S = 0; S < ns; ++S) {
+            uint64_t nx[2];
+            uint64_t lab[2];
+            int ne;
+            if (start[j] == ~0u) {
+                nx[0] = (S & emask) | ((S >> 1) & ~emask);
+                lab[0] = (cw0[S] >> j) & 1;
+                cw1[nx[0]] = cw0[S];
+                ne = 1;
+            } else {
+                uint64_t n0 = S, n1 = S ^ (1ull << na);
+                nx[0] = (n0 & emask) | ((n0 >> 1) & ~emask);
+                nx[1] = (n1 & emask) | ((n1 >> 1) & ~emask);
+                const uint64_t c1 = cw0[S] ^ M[start[j]];
+                cw1[nx[0]] = cw0[S];
+                cw1[nx[1]] = c1;
+                lab[0] = (cw0[S] >> j) & 1;
+                lab[1] = (c1 >> j) & 1;
+                ne = 2;
+            }
+            for (int e = 0; e < ne; ++e) {
+                const float sc = (lab[e] ^ HD) ? m0[S] + aY : m0[S];
+                if (sc < m1[nx[e]]) m1[nx[e]] = sc;
+            }
+        }
+        if (start[j] != ~0u) active[na++] = start[j];
+        if (end[j] != ~0u) {
+            memmove(active + B, active + B + 1, sizeof(unsigned) * (na - B));
+            --na;
+        }
+        { uint64_t *t = cw0; cw0 = cw1; cw1 = t; }
+        { float *t = m0; m0 = m1; m1 = t; }
+    }
+    const float r = m0[1] - m0[0];
+    free(cw0); free(cw1); free(m0); free(m1);
+    return r;
+}
+
+/* cosets of more than 2^plr_trellis_nfree words go through the trellis (tests set it to
+ * compare the two) */
+int plr_trellis_nfree = 12;
+
 float plr_minsum_llr(const plr_kernel *k, int phase, const float *y) {
     const int l = k->size, nfree = l - phase - 1;
+    if (nfree > plr_trellis_nfree) return trellis_minsum_llr(k, phase, y);
     uint32_t rows[PLR_MAXKERNEL];
     for (int r = 0; r < l; ++r) {
         rows[r] = 0;

@@ -37,7 +37,16 @@ constexpr int polar_rec_words(int K) { return K > 0 ? (K + 31) / 32 : 1; }
 // U / (ksize[0] ... ksize[λ-1]); per path S layer λ at soff[λ] (outer[λ] floats, λ >= 1), C
 // layer λ at coff[λ] (outer[λ] ksize[λ-1] bytes, C_0 = U), matrix offset states at ooff[j].
 constexpr int kPolarMaxKernel = 32;
-constexpr int kPolarMaxMatrixGpu = 16;  // coset enumeration 2^(size - 1 - phase) per LLR
+constexpr int kPolarMaxMatrixGpu = 32;  // as CTrellisKernelProcessor (< 64), rows as u32 masks
+// Matrix layers of size >= the trellis threshold (default 16, BCHK_POLAR_TRELLIS) take their
+// LLRs from CTrellisKernelProcessor's trellis (pull-form Viterbi over predecessor lists);
+// smaller ones enumerate the coset (2^(size - 1 - phase) words per LLR). Per (layer, phase):
+// tlog[(layer * kPolarMaxKernel + phase) * (kPolarMaxKernel + 1) + d] = log2 of the states at
+// depth d (d = 0..size), tbase[layer * kPolarMaxKernel + phase] = first entry of the phase in
+// tent; entries run depth by depth, one per state of depth d + 1, two 16-bit predecessors
+// (state | z << 13 | valid << 14).
+constexpr int kPolarTrellisMaxBits = 12;
+constexpr uint32_t kTrellisZ = 1u << 13, kTrellisValid = 1u << 14, kTrellisState = kTrellisZ - 1u;
 struct PolarMixedParams {
     const float *llr;
     uint8_t *info, *cw;
@@ -48,21 +57,28 @@ struct PolarMixedParams {
     const uint64_t *dfcorr;
     const int16_t *cwpos;
     const uint32_t *krows;  // [nl][kPolarMaxKernel]
+    const uint32_t *tent, *tbase;  // trellis predecessor lists (see above)
+    const uint8_t *tlog;
+    int32_t tstates;               // largest state count of any trellis layer (>= 64 if any)
     uint32_t B;
     int32_t nl, U, N, K, L;
     int32_t ssize, csize, osize;
     int32_t ksize[kPolarMaxLayers], outer[kPolarMaxLayers + 1];
     int32_t soff[kPolarMaxLayers + 1], coff[kPolarMaxLayers + 1], ooff[kPolarMaxLayers];
     uint8_t arikan[kPolarMaxLayers];
+    uint8_t trellis[kPolarMaxLayers];  // matrix layer decoded through its trellis
 };
 
-inline uint32_t polar_mixed_lds_bytes(int U, int L, int K, int ssize, int csize, int osize, int nl) {
+inline uint32_t polar_mixed_lds_bytes(int U, int L, int K, int ssize, int csize, int osize, int nl,
+                                      int tstates) {
     uint32_t b = (4u * (uint32_t)U + 15u) & ~15u;                                     // channel
     b += 4u * (uint32_t)ssize * (uint32_t)L + (uint32_t)csize * (uint32_t)L;           // S, C
     b = (b + (uint32_t)osize * (uint32_t)L + 15u) & ~15u;                              // offsets
     b = (b + 2u * (uint32_t)U + 15u) & ~15u;                                           // phases
     b += 4u * (uint32_t)kPolarMaxKernel * (uint32_t)nl;                                // rows
     b += 4u * (uint32_t)L + 4u * (uint32_t)L * (uint32_t)polar_rec_words(K);            // act, rec
+    b = (b + 15u) & ~15u;
+    b += 8u * (uint32_t)tstates;  // trellis state metrics: two buffers of tstates floats
     return (b + 15u) & ~15u;
 }
 

@@ -80,6 +80,9 @@ struct bchk_polar {
     std::vector<uint32_t> krows;  // [layer][kPolarMaxKernel]
     PolarMixedParams mp{};        // the mixed layout (sizes, offsets)
     size_t off_krows = 0;
+    std::vector<uint32_t> tent, tbase;  // matrix-layer trellises (polar_device.h)
+    std::vector<uint8_t> tlog;
+    size_t off_tent = 0, off_tbase = 0, off_tlog = 0;
     std::vector<int16_t> symmap, infopos, cwpos;
     std::vector<uint8_t> frozen;
     std::vector<int8_t> dfbit;
@@ -148,6 +151,113 @@ int read_kernel(const std::string &name, const char *kdir, int *size, uint32_t *
     *size = l;
     *arikan = false;
     return 0;
+}
+
+// CTrellisKernelProcessor's trellis of every phase of an l x l kernel (out/external/
+// TrellisKernelProcessor.cpp:69-179: MinimumSpan :7-67 of rows phase..l-1 with row `phase`
+// extended by a 1 at position l, states = active rows, state bits compressed as rows end),
+// stored as predecessor lists for the GPU's pull-form Viterbi (polar_device.h). Appends to
+// ent; base[phase], lg[phase * (kPolarMaxKernel + 1) + d]; returns the largest state count
+// (0 and a message when a depth needs more than 2^kPolarTrellisMaxBits states).
+int build_trellis(const uint32_t *rows, int l, std::vector<uint32_t> &ent, uint32_t *base, uint8_t *lg) {
+    int most = 1;
+    const unsigned N = (unsigned)l + 1u;
+    for (int ph = 0; ph < l; ++ph) {
+        const unsigned K = (unsigned)(l - ph);
+        uint64_t M[kPolarMaxKernel];
+        for (unsigned i = 0; i < K; ++i) M[i] = rows[ph + (int)i];
+        M[0] |= 1ull << l;
+        unsigned start[kPolarMaxKernel + 1], end[kPolarMaxKernel + 1];
+        for (unsigned c = 0; c < N; ++c) start[c] = end[c] = ~0u;
+        unsigned C = 0;  // MinimumSpan (:7-67)
+        for (unsigned i = 0; i < K; ++i) {
+            bool found = false;
+            for (; C < N; ++C) {
+                if (!((M[i] >> C) & 1ull)) {
+                    for (unsigned j = i + 1; j < K; ++j)
+                        if ((M[j] >> C) & 1ull) {
+                            M[i] ^= M[j];
+                            found = true;
+                            break;
+                        }
+                    if (found) {
+                        start[C] = i;
+                        break;
+                    }
+                } else {
+                    start[C] = i;
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) return pfail(BCHK_EINVAL, "Matrix is not full rank"), 0;
+            for (unsigned j = i + 1; j < K; ++j)
+                if ((M[j] >> C) & 1ull) M[j] ^= M[i];
+        }
+        for (int i = (int)K - 1; i >= 0; --i)
+            for (int j = (int)N - 1; j >= 0; --j)
+                if ((M[i] >> j) & 1ull) {
+                    end[j] = (unsigned)i;
+                    for (int q = 0; q < i; ++q)
+                        if ((M[q] >> j) & 1ull) M[q] ^= M[i];
+                    break;
+                }
+        base[ph] = (uint32_t)ent.size();
+        uint8_t *lgp = lg + (size_t)ph * (kPolarMaxKernel + 1);
+        lgp[0] = 0;
+        std::vector<uint64_t> cw0(1, 0ull), cw1;
+        unsigned active[kPolarMaxKernel + 1], na = 0;
+        for (int j = 0; j < l; ++j) {  // :107-158, depths 0..l-1 (GetLLRs never reads depth l's edges)
+            unsigned B = na;
+            for (unsigned q = 0; q < na; ++q)
+                if (active[q] == end[j]) { B = q; break; }
+            const uint64_t emask = (end[j] == ~0u) ? ~0ull : ((1ull << B) - 1ull);
+            const uint64_t ns = 1ull << na;
+            const unsigned na1 = na + (start[j] != ~0u ? 1u : 0u) - (end[j] != ~0u ? 1u : 0u);
+            if (na1 > (unsigned)kPolarTrellisMaxBits || na + 1 > (unsigned)kPolarTrellisMaxBits + 1)
+                return pfail(BCHK_EINVAL, "kernel of size %d: its trellis needs 2^%u states (GPU limit 2^%d)", l,
+                             std::max(na1, na), kPolarTrellisMaxBits), 0;
+            const uint64_t ns1 = 1ull << na1;
+            cw1.assign(ns1, 0ull);
+            const size_t e0 = ent.size();
+            ent.resize(e0 + ns1, 0u);
+            auto link = [&](uint64_t S, uint64_t S1, uint32_t z) {
+                uint32_t &e = ent[e0 + S1];
+                const uint32_t h = (uint32_t)S | (z ? kTrellisZ : 0u) | kTrellisValid;
+                if (!(e & kTrellisValid)) e |= h;
+                else e |= h << 16;
+            };
+            if (start[j] == ~0u) {
+                for (uint64_t S = 0; S < ns; ++S) {
+                    const uint32_t bit = (uint32_t)((cw0[S] >> j) & 1ull);
+                    const uint64_t nx = (S & emask) | ((S >> 1) & ~emask);
+                    cw1[nx] = cw0[S];
+                    link(S, nx, bit);
+                }
+            } else {
+                for (uint64_t S = 0; S < ns; ++S) {
+                    uint64_t n0 = S, n1 = S ^ (1ull << na);
+                    n0 = (n0 & emask) | ((n0 >> 1) & ~emask);
+                    n1 = (n1 & emask) | ((n1 >> 1) & ~emask);
+                    const uint64_t c1 = cw0[S] ^ M[start[j]];
+                    cw1[n0] = cw0[S];
+                    cw1[n1] = c1;
+                    link(S, n0, (uint32_t)((cw0[S] >> j) & 1ull));
+                    link(S, n1, (uint32_t)((c1 >> j) & 1ull));
+                }
+                active[na++] = start[j];
+            }
+            cw0.swap(cw1);
+            if (end[j] != ~0u) {
+                memmove(active + B, active + B + 1, sizeof(unsigned) * (na - B));
+                --na;
+            }
+            if (na != na1) return pfail(BCHK_EINVAL, "trellis construction inconsistent"), 0;
+            lgp[j + 1] = (uint8_t)na;
+            most = std::max(most, 1 << na);
+        }
+    }
+    return most;
 }
 
 int parse_spec(bchk_polar *c, const char *spec, const char *kdir) {
@@ -269,7 +379,27 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
         m.ssize = (so + 3) & ~3;
         m.csize = (co + 15) & ~15;
         m.osize = (oo + 15) & ~15;
-        c->lds = polar_mixed_lds_bytes(c->U, c->L, c->K, m.ssize, m.csize, m.osize, nl);
+        // matrix layers from the trellis threshold up take their LLRs from the trellis
+        int tmin = 16;
+        if (const char *e = getenv("BCHK_POLAR_TRELLIS")) tmin = std::max(2, atoi(e));
+        m.tstates = 0;
+        c->tbase.assign((size_t)nl * kPolarMaxKernel, 0u);
+        c->tlog.assign((size_t)nl * kPolarMaxKernel * (kPolarMaxKernel + 1), 0u);
+        c->tent.clear();
+        for (int j = 0; j < nl; ++j) {
+            m.trellis[j] = (!c->arikan[j] && c->ksize[j] >= tmin) ? 1 : 0;
+            if (!m.trellis[j]) continue;
+            const int most = build_trellis(&c->krows[(size_t)j * kPolarMaxKernel], c->ksize[j], c->tent,
+                                           &c->tbase[(size_t)j * kPolarMaxKernel],
+                                           &c->tlog[(size_t)j * kPolarMaxKernel * (kPolarMaxKernel + 1)]);
+            if (!most) {
+                delete c;
+                return BCHK_EINVAL;  // build_trellis set the message
+            }
+            m.tstates = std::max(m.tstates, std::max(64, most));
+        }
+        if (c->tent.empty()) c->tent.push_back(0u);
+        c->lds = polar_mixed_lds_bytes(c->U, c->L, c->K, m.ssize, m.csize, m.osize, nl, m.tstates);
     } else {
         c->lds = polar_lds_bytes(c->U, c->L, c->K);
     }
@@ -305,6 +435,9 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
     c->off_cwpos = o; o = al(o + 2 * (size_t)c->N);
     c->off_dfcorr = o; o = al(o + 8 * (size_t)c->U);
     c->off_krows = o; o = al(o + 4 * c->krows.size());
+    c->off_tent = o; o = al(o + 4 * c->tent.size());
+    c->off_tbase = o; o = al(o + 4 * c->tbase.size());
+    c->off_tlog = o; o = al(o + c->tlog.size());
     std::vector<uint8_t> blob(o, 0);
     memcpy(blob.data() + c->off_symmap, c->symmap.data(), 2 * (size_t)c->U);
     {
@@ -316,6 +449,9 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
     memcpy(blob.data() + c->off_cwpos, c->cwpos.data(), 2 * (size_t)c->N);
     memcpy(blob.data() + c->off_dfcorr, c->dfcorr.data(), 8 * (size_t)c->U);
     memcpy(blob.data() + c->off_krows, c->krows.data(), 4 * c->krows.size());
+    if (!c->tent.empty()) memcpy(blob.data() + c->off_tent, c->tent.data(), 4 * c->tent.size());
+    if (!c->tbase.empty()) memcpy(blob.data() + c->off_tbase, c->tbase.data(), 4 * c->tbase.size());
+    if (!c->tlog.empty()) memcpy(blob.data() + c->off_tlog, c->tlog.data(), c->tlog.size());
     if (hipMalloc(&c->d_tab, o) != hipSuccess ||
         hipMemcpy(c->d_tab, blob.data(), o, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -393,6 +529,9 @@ int bchk_polar_decode_device(bchk_polar *c, const float *d_llr, size_t B, uint8_
         m.dfcorr = p.dfcorr;
         m.cwpos = p.cwpos;
         m.krows = reinterpret_cast<const uint32_t *>(c->d_tab + c->off_krows);
+        m.tent = reinterpret_cast<const uint32_t *>(c->d_tab + c->off_tent);
+        m.tbase = reinterpret_cast<const uint32_t *>(c->d_tab + c->off_tbase);
+        m.tlog = c->d_tab + c->off_tlog;
         m.B = p.B;
         m.U = c->U;
         m.N = c->N;

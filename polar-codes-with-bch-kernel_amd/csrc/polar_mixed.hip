@@ -103,6 +103,7 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
     const int o_ph = (o_O + p.osize * L + 15) & ~15;
     const int o_rows = (o_ph + 2 * U + 15) & ~15;
     const int o_act = o_rows + 4 * kPolarMaxKernel * nl;
+    const int o_tm = (o_act + 4 * L + 4 * L * RW + 15) & ~15;
     float *chan = reinterpret_cast<float *>(smem);
     float *S = reinterpret_cast<float *>(smem + o_S);
     uint8_t *C = smem + o_C;
@@ -111,6 +112,7 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
     uint32_t *rows = reinterpret_cast<uint32_t *>(smem + o_rows);  // [layer][row] bitmasks
     uint32_t *act = reinterpret_cast<uint32_t *>(smem + o_act);
     uint32_t *rec = act + L;
+    float *tmet = reinterpret_cast<float *>(smem + o_tm);  // trellis state metrics, 2 x tstates
     const bool mine = lane < L;
     for (int i = lane; i < U; i += 64) ph[i] = p.phase[i];
     for (int i = lane; i < kPolarMaxKernel * nl; i += 64) rows[i] = p.krows[i];
@@ -189,6 +191,63 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                     }
                 }
                 wsync();
+                if (p.trellis[j]) {
+                    // CTrellisKernelProcessor::GetLLRs (:260-292) as a pull-form Viterbi: a state
+                    // of depth dd + 1 takes the smaller of its (at most two) predecessors' metrics,
+                    // each plus |Y| when its edge label differs from the hard decision (min
+                    // commutes with the monotone float add, so the values are the reference's).
+                    // G lanes per item (G = states of the phase's widest depth, at most 64).
+                    const int tp = j * kPolarMaxKernel + loc;
+                    const uint8_t *lgp = p.tlog + (size_t)tp * (kPolarMaxKernel + 1);
+                    const uint32_t *ent0 = p.tent + p.tbase[tp];
+                    int ab = 0;
+                    for (int dd = 1; dd <= l; ++dd) ab = lgp[dd] > ab ? lgp[dd] : ab;
+                    const int stride = 1 << ab, G = stride < 64 ? stride : 64, ipr = 64 / G;
+                    const int slot = lane / G, sub = lane % G;
+                    for (int base = 0; base < tot; base += ipr) {
+                        const int it = base + slot;
+                        const bool have = slot < ipr && it < tot;
+                        int q = 0, s = 0;
+                        if (have) {
+                            q = (int)act[it / d];
+                            s = it % d;
+                        }
+                        const float *src = Sof(q, j);
+                        const uint8_t *off = Oof(q, j);
+                        float *m0 = tmet + slot * stride, *m1 = tmet + p.tstates + slot * stride;
+                        if (have && sub == 0) m0[0] = 0.0f;
+                        wsync();
+                        const uint32_t *e = ent0;
+                        for (int dd = 0; dd < l; ++dd) {
+                            const int n1 = 1 << lgp[dd + 1];
+                            if (have) {
+                                const float v = src[dd * d + s];
+                                const float yv = off[dd * d + s] ? -v : v;
+                                const bool hd = yv < 0.0f;  // HD = Y < 0 (:270)
+                                const float ay = fabsf(yv);
+                                for (int S1 = sub; S1 < n1; S1 += G) {
+                                    const uint32_t w = e[S1], a = w & 0xFFFFu, b = w >> 16;
+                                    float x = m0[a & kTrellisState];
+                                    if (((a & kTrellisZ) != 0u) != hd) x = x + ay;
+                                    if (b & kTrellisValid) {
+                                        float xb = m0[b & kTrellisState];
+                                        if (((b & kTrellisZ) != 0u) != hd) xb = xb + ay;
+                                        x = xb < x ? xb : x;
+                                    }
+                                    m1[S1] = x;
+                                }
+                            }
+                            wsync();
+                            float *tt = m0;
+                            m0 = m1;
+                            m1 = tt;
+                            e += n1;
+                        }
+                        if (have && sub == 0) Sof(q, j + 1)[s] = m0[1] - m0[0];  // (:292)
+                        wsync();
+                    }
+                    continue;
+                }
                 // lanes per item: the coset split when items are fewer than lanes
                 int lpi = 1;
                 const int nfree = l - loc - 1;

@@ -88,8 +88,25 @@ def _bch_kernel(power, prim):
     return M
 
 
+def _field_order(K, power, prim):
+    """swapColumns' reordering (root bchCoder.cpp:478-496): column i >= 3 takes the column
+    of the field element i (column j + 1 holds alpha^j)."""
+    n = 1 << power
+    el, x = [], 1
+    for _ in range(n - 1):
+        el.append(x)
+        x <<= 1
+        if x >> power:
+            x ^= prim
+    F = K.copy()
+    for i in range(3, n):
+        F[:, i] = K[:, el.index(i) + 1]
+    return F
+
+
 KERNELS = {
     "bch8": _bch_kernel(3, 0b1011),
+    "bch32f": _field_order(_bch_kernel(5, 0b100101), 5, 0b100101),  # trellis: 2^12 states
     "bch16": _bch_kernel(4, 0b10011),
     "k4": np.array([[1, 0, 0, 0], [1, 0, 1, 0], [1, 1, 0, 0], [1, 1, 1, 1]], np.uint8),
     "a2": np.array([[1, 0], [1, 1]], np.uint8),
@@ -151,8 +168,12 @@ def test_spec_errors_before_the_device(kdir, tmp_path):
     F = load()
     (tmp_path / "sing.txt").write_text("3\n1 0 0\n1 0 0\n0 1 1\n")
     (tmp_path / "big.txt").write_text(_kernel_text(_lower_kernel(20, 1)))
-    for name, msg in [("sing", "singular"), ("big", "sizes up to 16"), ("missing", "Error reading kernel file")]:
-        spec = f"20 10 0 1 0 0\n-{name}.txt\n" + "".join(f"1 {i}\n" for i in range(10))
+    (tmp_path / "wide.txt").write_text(_kernel_text(_lower_kernel(32, 1)))
+    (tmp_path / "huge.txt").write_text("40\n" + "\n".join(" ".join("1" if c <= r else "0" for c in range(40))
+                                                         for r in range(40)) + "\n")
+    for name, msg, n in [("sing", "singular", 3), ("wide", "GPU limit", 32), ("huge", "size", 40),
+                         ("missing", "Error reading kernel file", 20)]:
+        spec = f"{n} {n // 2} 0 1 0 0\n-{name}.txt\n" + "".join(f"1 {i}\n" for i in range(n - n // 2))
         with pytest.raises(F.BchkError, match=msg):
             F.PolarListDecoder(spec, 4, kernel_dir=str(tmp_path))
     with pytest.raises(F.BchkError, match="Unknown kernel"):
@@ -169,6 +190,11 @@ CODES = [
     (("bch16", "A"), 16, 2, ()),        # the reference's 16 x 16 extended-BCH kernel
     (("A", "bch8", "A"), 16, 2, (3,)),  # its 8 x 8 one, between Arikan layers
     (("bch16", "bch8"), 64, 4, ()),     # two BCH kernels, U = 128
+]
+# 32 x 32: the extended-BCH kernel in field-element order, through its trellis
+CODES32 = [
+    (("bch32f", "A"), 32, 2, ()),
+    (("A", "bch32f"), 30, 2, (7,)),
 ]
 
 
@@ -213,3 +239,77 @@ def test_matrix_arikan_kernel_equals_the_arikan_decoder(kdir):
     info = np.random.default_rng(1).integers(0, 2, (64, 28)).astype(np.uint8)
     llr = awgn_llr(o.encode(info), 1.5, 28 / 64, seed=8)
     _same(dm.decode(llr), da.decode(llr))
+
+
+def _plr_kernel(K):
+    import ctypes as C
+
+    class PK(C.Structure):
+        _fields_ = [("size", C.c_int), ("arikan", C.c_int), ("K", C.c_uint8 * 1024), ("Kinv", C.c_uint8 * 1024)]
+
+    k = PK()
+    k.size, k.arikan = len(K), 0
+    for i, v in enumerate(np.asarray(K, np.uint8).ravel()):
+        k.K[i] = int(v)
+    return k
+
+
+@pytest.mark.parametrize("name", ["k3", "k4", "k8", "bch8", "k16", "bch16"])
+def test_oracle_trellis_equals_coset_enumeration(name):
+    """The oracle's literal trellis (TrellisKernelProcessor.cpp:69-294, used for large
+    cosets) against its coset enumeration, bit for bit in float, every phase."""
+    import ctypes as C
+    from polar_lib import lib as plib
+    L = plib()
+    L.plr_minsum_llr.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    L.plr_minsum_llr.restype = C.c_float
+    thr = C.c_int.in_dll(L, "plr_trellis_nfree")
+    K = KERNELS[name]
+    k = _plr_kernel(K)
+    rng = np.random.default_rng(len(K))
+    old = thr.value
+    try:
+        for _ in range(4):
+            y = rng.normal(0, 1.5, len(K)).astype(np.float32)
+            for ph in range(len(K)):
+                thr.value = 64
+                a = L.plr_minsum_llr(C.byref(k), ph, y.ctypes.data_as(C.c_void_p))
+                thr.value = -1
+                b = L.plr_minsum_llr(C.byref(k), ph, y.ctypes.data_as(C.c_void_p))
+                assert np.float32(a).view(np.uint32) == np.float32(b).view(np.uint32), (name, ph, a, b)
+    finally:
+        thr.value = old
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layers,K,dyn,punct", CODES, ids=["-".join(c[0]) for c in CODES])
+@pytest.mark.parametrize("L", [1, 4, 8])
+def test_gpu_mixed_trellis_everywhere_matches_oracle(kdir, layers, K, dyn, punct, L, monkeypatch):
+    """Every matrix layer (3 x 3 up) through its trellis (BCHK_POLAR_TRELLIS=2) instead of
+    the coset enumeration: same lists, bit for bit."""
+    monkeypatch.setenv("BCHK_POLAR_TRELLIS", "2")
+    spec = mixed_spec(layers, K, dyn, punct, seed=len(layers) * 11 + K)
+    o = PolarOracle(spec, kdir)
+    d = load().PolarListDecoder(spec, L, kernel_dir=kdir)
+    rng = np.random.default_rng(L + K + 1)
+    info = rng.integers(0, 2, (24, K)).astype(np.uint8)
+    cw = o.encode(info)
+    for snr in (0.0, 2.0):
+        llr = awgn_llr(cw, snr, K / o.N, seed=int(snr * 10) + L + 3)
+        _same(d.decode(llr), o.decode_batch(llr, L))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layers,K,dyn,punct", CODES32, ids=["-".join(c[0]) for c in CODES32])
+@pytest.mark.parametrize("L", [1, 4])
+def test_gpu_mixed_32x32_kernel_matches_oracle(kdir, layers, K, dyn, punct, L):
+    spec = mixed_spec(layers, K, dyn, punct, seed=len(layers) * 13 + K)
+    o = PolarOracle(spec, kdir)
+    d = load().PolarListDecoder(spec, L, kernel_dir=kdir)
+    rng = np.random.default_rng(L + K)
+    info = rng.integers(0, 2, (12, K)).astype(np.uint8)
+    cw = o.encode(info)
+    np.testing.assert_array_equal(d.encode(info), cw)
+    for snr in (1.0, 3.0):
+        llr = awgn_llr(cw, snr, K / o.N, seed=int(snr * 10) + L)
+        _same(d.decode(llr), o.decode_batch(llr, L))
