@@ -730,7 +730,7 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
     nd.pad = 0;
     bool have = lane == 0 && t >= 1;
     int sp = 0, np = 0;  // stack and pending-emission counts
-    uint32_t nodes = 1, steps = 0;
+    uint32_t steps = 0;
     const uint64_t below = (1ull << lane) - 1ull;
     for (;;) {
         const uint64_t idle = ballot(!have);

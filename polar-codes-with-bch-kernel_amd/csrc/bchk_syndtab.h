@@ -24,7 +24,7 @@
 // lookup in the common case, mostly L2 / Infinity-Cache resident while the search kernels
 // run. Built once per (m, t) on the host, uploaded once per device.
 //
-// tests/test_filter.py checks every lookup against the oracle's Decoder::decode (the small
+// tests/test_syndtab.py checks every lookup against the oracle's Decoder::decode (the small
 // codes exhaustively); tests/test_gpu_parity.py runs every path with and without it.
 #pragma once
 #include <stdint.h>

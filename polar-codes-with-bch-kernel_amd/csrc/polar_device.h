@@ -21,6 +21,8 @@ struct PolarParams {
     const int16_t *cwpos;   // [N] transmitted (neither shortened nor punctured) symbols
     uint32_t B;
     int32_t n, U, N, K, L;
+    int32_t pathCw;                       // packed partial-sum words per path
+    int32_t cwoff[kPolarMaxLayers + 1];   // word offset of C_λ in a path's packed array
 };
 
 constexpr uint16_t kPhaseFrozen = 1u, kPhaseCorr = 0x100u;
@@ -82,16 +84,32 @@ inline uint32_t polar_mixed_lds_bytes(int U, int L, int K, int ssize, int csize,
     return (b + 15u) & ~15u;
 }
 
-// LDS bytes of one wave's state (see polar_sclist.hip): channel LLRs, per path S and C,
-// the phase table, the active-path list and per path the information bits decided so far.
+// Packed partial sums of the all-Arikan kernel (polar_sclist.hip): per path C_0 (U bits,
+// the codeword) then C_λ (U >> (λ-1) bits, λ = 1..n), each starting on a 32-bit word; the
+// path stride is odd, so the same word of different paths falls in different banks. Writes
+// the word offsets (n + 1 entries) when off is given; returns the stride in words.
+inline int polar_cw_layout(int U, int32_t *off) {
+    int n = 0;
+    while ((1 << n) < U) ++n;
+    int w = 0;
+    for (int lam = 0; lam <= n; ++lam) {
+        if (off) off[lam] = w;
+        const int bits = lam == 0 ? U : (U >> (lam - 1));
+        w += (bits + 31) / 32;
+    }
+    return w | 1;
+}
+
+// LDS bytes of one wave's state (see polar_sclist.hip): per path S (floats) and the packed
+// partial sums, the active-path list and per path the information bits decided so far. The
+// channel LLRs and the phase table are read from global memory (layer 0 is read at two
+// phases per codeword, the phase word once per phase).
 inline uint32_t polar_lds_bytes(int U, int L, int K) {
-    uint32_t b = (4u * (uint32_t)U + 15u) & ~15u;                     // channel
-    b += 4u * (uint32_t)polar_path_s(U) * (uint32_t)L;                // S
-    b += (uint32_t)polar_path_c(U) * (uint32_t)L;                     // C
-    b += 2u * (uint32_t)U;                                            // phase table
+    uint32_t b = 4u * (uint32_t)polar_path_s(U) * (uint32_t)L;             // S
+    b += 4u * (uint32_t)polar_cw_layout(U, nullptr) * (uint32_t)L;          // C (bits)
     b = (b + 15u) & ~15u;
-    b += 4u * (uint32_t)L;                                            // active list
-    b += 4u * (uint32_t)L * (uint32_t)polar_rec_words(K);             // information bits
+    b += 4u * (uint32_t)L;                                                  // active list
+    b += 4u * (uint32_t)L * (uint32_t)polar_rec_words(K);                   // information bits
     return (b + 15u) & ~15u;
 }
 

@@ -468,7 +468,7 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
     c->grid = per_cu * prop.multiProcessorCount;
     if (const char *g = getenv("BCHK_POLAR_GRID")) c->grid = std::max(1, atoi(g));
     if (getenv("BCHK_POLAR_DEBUG"))
-        fprintf(stderr, "bchk_polar: U=%d L=%d lds=%u per_cu=%d CUs=%d grid=%d\n", c->U, c->L, c->lds, per_cu,
+        fprintf(stderr, "bchk_polar: U=%d L=%d lds=%zu per_cu=%d CUs=%d grid=%d\n", c->U, c->L, c->lds, per_cu,
                 prop.multiProcessorCount, c->grid);
     *out = c;
     return 0;
@@ -511,6 +511,7 @@ int bchk_polar_decode_device(bchk_polar *c, const float *d_llr, size_t B, uint8_
     p.cwpos = reinterpret_cast<const int16_t *>(c->d_tab + c->off_cwpos);
     p.dfcorr = reinterpret_cast<const uint64_t *>(c->d_tab + c->off_dfcorr);
     p.B = (uint32_t)B;
+    p.pathCw = polar_cw_layout(c->U, p.cwoff);
     p.n = c->n;
     p.U = c->U;
     p.N = c->N;

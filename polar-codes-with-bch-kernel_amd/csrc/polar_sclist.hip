@@ -10,8 +10,10 @@
 //
 // Execution model: one 64-lane wave per codeword (persistent over the batch).
 //   * LDS holds every path's LLRs S_λ (U >> λ floats) and partial sums C_λ (kernel inputs
-//     of the current block, U >> (λ-1) bytes; C_0 = the codeword), the phase table and the
-//     information bits decided so far (packed, flushed every 32 decisions).
+//     of the current block, U >> (λ-1) bits packed in 32-bit words, each layer word-aligned;
+//     C_0 = the codeword) and the information bits decided so far (packed, flushed every 32
+//     decisions). The channel LLRs (read at two phases per codeword) and the phase table
+//     come from global memory, so (1024, 512) at L = 8 fits 4 waves per CU.
 //   * Lane q < L holds path q's scalar state in registers: metric R, leaf LLR, dynamic-
 //     freezing mask, the current record word and slot q of the path-index stack (pushes and
 //     pops are v_writelane / v_readlane on a wave-uniform top).
@@ -39,11 +41,8 @@ __device__ __forceinline__ void wave_sync_p() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// offsets inside one path's arrays: S_λ (λ >= 1) and C_λ
+// offset of S_λ (λ >= 1) inside one path's LLR array
 __device__ __forceinline__ int s_off(int U, int lam) { return U - (U >> (lam - 1)); }
-__device__ __forceinline__ int c_off(int U, int lam) {
-    return lam == 0 ? 0 : (lam == 1 ? U : 3 * U - (U >> (lam - 2)));
-}
 
 // SoftXOR (SoftProcessing.cpp:54-80): sign(a) sign(b) min(|a|, |b|)
 __device__ __forceinline__ float f_minsum(float a, float b) {
@@ -101,34 +100,32 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = (int)threadIdx.x;
     const int U = p.U, n = p.n, L = p.L, K = p.K;
-    const int pathS = polar_path_s(U), pathC = polar_path_c(U), RW = polar_rec_words(K);
+    const int pathS = polar_path_s(U), pathC = p.pathCw, RW = polar_rec_words(K);
     // LDS layout: polar_lds_bytes (polar_device.h)
     // (byte offsets from smem, never through integer casts of the pointers, which would
     // lose the LDS address space and turn every access into a FLAT one)
-    const int o_S = (4 * U + 15) & ~15;
-    const int o_C = o_S + 4 * pathS * L;
-    const int o_ph = o_C + pathC * L;
-    const int o_act = (o_ph + 2 * U + 15) & ~15;
-    float *chan = reinterpret_cast<float *>(smem);
-    float *S = reinterpret_cast<float *>(smem + o_S);
-    uint8_t *C = smem + o_C;
-    uint16_t *ph = reinterpret_cast<uint16_t *>(smem + o_ph);
+    const int o_C = 4 * pathS * L;
+    const int o_act = (o_C + 4 * pathC * L + 15) & ~15;
+    float *S = reinterpret_cast<float *>(smem);
+    uint32_t *C = reinterpret_cast<uint32_t *>(smem + o_C);  // packed bits, words per path
     uint32_t *act = reinterpret_cast<uint32_t *>(smem + o_act);
     uint32_t *rec = act + L;
-    const int lastc = c_off(U, n);  // C_n: the two inputs of the last Arikan block
+    const int lastc = p.cwoff[n];  // C_n: the two inputs of the last Arikan block (one word)
     const bool mine = lane < L;
-
-    for (int i = lane; i < U; i += 64) ph[i] = p.phase[i];
+    auto cbit = [&](int q, int lam, int s) -> uint32_t {
+        const int b = s;
+        return (C[(size_t)q * pathC + p.cwoff[lam] + (b >> 5)] >> (b & 31)) & 1u;
+    };
 
     PathStack st;
     st.slot = 0;
     for (uint32_t cw = blockIdx.x; cw < p.B; cw += gridDim.x) {
-        // ---- LoadLLRs (MixedKernelEncoder.cpp:181-207)
+        // ---- LoadLLRs (MixedKernelEncoder.cpp:181-207), applied where layer 0 is read
         const float *y = p.llr + (size_t)cw * p.N;
-        for (int i = lane; i < U; i += 64) {
+        auto chan = [&](int i) -> float {
             const int m = p.symmap[i];
-            chan[i] = m >= 0 ? y[m] : (m == -1 ? 100000.0f : 0.0f);
-        }
+            return m >= 0 ? y[m] : (m == -1 ? 100000.0f : 0.0f);
+        };
         // ---- Cleanup + AssignInitialPath (TVMemoryEngine.cpp:58-94)
         st.reset(L, lane);
         const uint32_t pid = st.pop(lane);
@@ -141,7 +138,7 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
         int nact = list_active(active, act, lane, L);
 
         for (int phi = 0; phi < U; ++phi) {
-            const uint32_t e = __builtin_amdgcn_readfirstlane((uint32_t)ph[phi]);
+            const uint32_t e = __builtin_amdgcn_readfirstlane((uint32_t)p.phase[phi]);
             // ---- IterativelyCalcS (KernelListEngine.cpp:370-447): from layer m, where the
             // block of phase phi starts, down to the single LLR of layer n
             int m = 0, local = 0;
@@ -156,12 +153,19 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
                 const int tot = nact << lgd;
                 for (int it = lane; it < tot; it += 64) {
                     const int q = (int)act[it >> lgd], s = it & (d - 1);
-                    const float *src = (j == 0) ? chan : S + (size_t)q * pathS + s_off(U, j);
                     float *dst = S + (size_t)q * pathS + s_off(U, j + 1);
-                    const float a = src[s], b = src[d + s];
+                    float a, b;
+                    if (j == 0) {
+                        a = chan(s);
+                        b = chan(d + s);
+                    } else {
+                        const float *src = S + (size_t)q * pathS + s_off(U, j);
+                        a = src[s];
+                        b = src[d + s];
+                    }
                     float r;
                     if (loc) {  // SoftCombine (:39-50): b - a if u = 1 else b + a
-                        r = C[(size_t)q * pathC + c_off(U, j + 1) + s] ? b - a : b + a;
+                        r = cbit(q, j + 1, s) ? b - a : b + a;
                     } else {
                         r = f_minsum(a, b);
                     }
@@ -212,27 +216,27 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
                     const int l1 = (int)st.pop(lane);  // ClonePath: copy the live state of l
                     {
                         // S_j (j >= 1) is read again iff bit n-1-j of phi is 0; copy from the
-                        // first such layer on. Left halves of C_λ are pending iff bit n-λ of
-                        // phi is 1; copy from the first such λ on.
+                        // first such layer on. The packed partial sums are copied whole
+                        // (3U bits).
                         const uint32_t zs = ~(uint32_t)phi & ((1u << (n - 1)) - 1u);
                         const int s0 = zs ? (s_off(U, n - 1 - (31 - __builtin_clz(zs))) & ~3) : pathS;
                         const int ns4 = (((U + 3) & ~3) - s0) >> 2;
-                        const int c0 = phi ? (c_off(U, n - (31 - __builtin_clz((uint32_t)phi))) & ~15) : pathC;
-                        const int nc16 = (((3 * U + 15) & ~15) - c0) >> 4;
+                        const int nc = pathC;
                         const int nr = k >> 5;
                         const uint4 *sS = reinterpret_cast<const uint4 *>(S + (size_t)l * pathS + s0);
                         uint4 *dS = reinterpret_cast<uint4 *>(S + (size_t)l1 * pathS + s0);
-                        const uint4 *sC = reinterpret_cast<const uint4 *>(C + (size_t)l * pathC + c0);
-                        uint4 *dC = reinterpret_cast<uint4 *>(C + (size_t)l1 * pathC + c0);
-                        const int top = ns4 > nc16 ? ns4 : nc16;
-                        for (int i = lane; i < top || i < nr; i += 64) {
-                            uint4 vs, vc;
-                            uint32_t vr = 0;
+                        const uint32_t *sC = C + (size_t)l * pathC;
+                        uint32_t *dC = C + (size_t)l1 * pathC;
+                        int top = ns4 > nc ? ns4 : nc;
+                        top = top > nr ? top : nr;
+                        for (int i = lane; i < top; i += 64) {
+                            uint4 vs;
+                            uint32_t vc = 0, vr = 0;
                             if (i < ns4) vs = sS[i];
-                            if (i < nc16) vc = sC[i];
+                            if (i < nc) vc = sC[i];
                             if (i < nr) vr = rec[l * RW + i];
                             if (i < ns4) dS[i] = vs;
-                            if (i < nc16) dC[i] = vc;
+                            if (i < nc) dC[i] = vc;
                             if (i < nr) rec[l1 * RW + i] = vr;
                         }
                     }
@@ -251,8 +255,10 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
                 wave_sync_p();
             }
             const bool now = mine && ((active >> lane) & 1u);
-            if (now) {
-                C[(size_t)lane * pathC + lastc + (phi & 1)] = (uint8_t)dec;
+            if (now) {  // the path's own word: no other lane writes it
+                uint32_t &w = C[(size_t)lane * pathC + lastc];
+                const uint32_t bit = 1u << (phi & 1);
+                w = dec ? (w | bit) : (w & ~bit);
                 if (dec) dm ^= corr;
             }
             if (!(e & kPhaseFrozen)) {
@@ -275,14 +281,29 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
                     const int psi = ph2 >> 1;
                     const int stride = 1 << lgs, next = stride << 1;
                     const int phi0 = (lam > 1) ? (psi & 1) * next : 0;
-                    const int tot = nact << lgs;
-                    for (int it = lane; it < tot; it += 64) {
-                        const int q = (int)act[it >> lgs], s = it & (stride - 1);
-                        const uint8_t *src = C + (size_t)q * pathC + c_off(U, lam);
-                        uint8_t *dst = C + (size_t)q * pathC + c_off(U, lam - 1) + phi0;
-                        const uint8_t x0 = src[s], x1 = src[stride + s];
-                        dst[s] = (uint8_t)(x0 ^ x1);
-                        dst[stride + s] = x1;
+                    if (stride >= 32) {  // whole words: (x0, x1) -> (x0 ^ x1, x1), 32 at a time
+                        const int lw = lgs - 5, sw = 1 << lw, tot = nact << lw;
+                        for (int it = lane; it < tot; it += 64) {
+                            const int q = (int)act[it >> lw], s = it & (sw - 1);
+                            const uint32_t *src = C + (size_t)q * pathC + p.cwoff[lam];
+                            uint32_t *dst = C + (size_t)q * pathC + p.cwoff[lam - 1] + (phi0 >> 5);
+                            const uint32_t x0 = src[s], x1 = src[sw + s];
+                            dst[s] = x0 ^ x1;
+                            dst[sw + s] = x1;
+                        }
+                    } else if (mine && ((active >> lane) & 1u)) {  // one word per path, its lane
+                        const uint32_t v = C[(size_t)lane * pathC + p.cwoff[lam]];
+                        const uint32_t mk = (1u << stride) - 1u;
+                        const uint32_t x0 = v & mk, x1 = (v >> stride) & mk;
+                        const uint32_t r = (x0 ^ x1) | (x1 << stride);  // 2 stride bits
+                        uint32_t &w = C[(size_t)lane * pathC + p.cwoff[lam - 1] + (phi0 >> 5)];
+                        if (next == 32) {
+                            w = r;
+                        } else {
+                            const int sh = phi0 & 31;
+                            const uint32_t m2 = ((1u << next) - 1u) << sh;
+                            w = (w & ~m2) | (r << sh);
+                        }
                     }
                     wave_sync_p();
                     ++lgs;
@@ -304,7 +325,7 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
         }
         for (int r = 0; r < nact; ++r) {
             const int q = (int)__builtin_ctzll(__ballot(me && rk == r));
-            const uint8_t *cq = C + (size_t)q * pathC;  // C_0: the unshortened codeword
+            const uint32_t *cq = C + (size_t)q * pathC;  // C_0: the unshortened codeword (bits)
             const uint32_t *rq = rec + q * RW;
             const size_t row = (size_t)cw * L + r;
             if ((K & 3) == 0) {  // information bits, four per lane and store
@@ -321,11 +342,15 @@ __global__ void __launch_bounds__(64) polar_sclist_kernel(PolarParams p) {
                     uint32_t *o4 = reinterpret_cast<uint32_t *>(p.cw + row * p.N);
                     for (int w = lane; w < (p.N >> 2); w += 64) {
                         const int i0 = 4 * w;
-                        o4[w] = (uint32_t)cq[p.cwpos[i0]] | ((uint32_t)cq[p.cwpos[i0 + 1]] << 8) |
-                                ((uint32_t)cq[p.cwpos[i0 + 2]] << 16) | ((uint32_t)cq[p.cwpos[i0 + 3]] << 24);
+                        auto bitat = [&](int i) { return (cq[i >> 5] >> (i & 31)) & 1u; };
+                        o4[w] = bitat(p.cwpos[i0]) | (bitat(p.cwpos[i0 + 1]) << 8) |
+                                (bitat(p.cwpos[i0 + 2]) << 16) | (bitat(p.cwpos[i0 + 3]) << 24);
                     }
                 } else {
-                    for (int i = lane; i < p.N; i += 64) p.cw[row * p.N + i] = cq[p.cwpos[i]];
+                    for (int i = lane; i < p.N; i += 64) {
+                        const int ci = p.cwpos[i];
+                        p.cw[row * p.N + i] = (uint8_t)((cq[ci >> 5] >> (ci & 31)) & 1u);
+                    }
                 }
             }
             if (lane == 0) p.metric[row] = rdl_f(R, q);
