@@ -1436,8 +1436,13 @@ __device__ uint32_t tail_dequeue(const SearchParams &p, uint32_t &item) {
     return kEmptySlot;
 }
 
+#ifdef BCHK_SEARCH_WPE  // experiment builds (make wpe): waves per SIMD the registers must allow
+#define BCHK_SEARCH_ATTR __attribute__((amdgpu_waves_per_eu(BCHK_SEARCH_WPE)))
+#else
+#define BCHK_SEARCH_ATTR
+#endif
 template <int M, int TMAX, bool TAB, bool AN>
-__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock)
+__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) BCHK_SEARCH_ATTR
 kaneko_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
