@@ -18,6 +18,7 @@
 // queue that the wave-per-codeword kernel (bchk_kernels.hip) processes from scratch, so
 // every result is the reference's.
 #include <algorithm>
+#include <cstdlib>
 
 #include "bchk_core.h"
 #include "bchk_launch.h"
@@ -30,6 +31,49 @@ constexpr int kSlice = 8;
 constexpr int kFastWaves = 8;  // waves per persistent block
 constexpr int kStageBytes = 64 * kRowD * 8;
 }  // namespace
+
+// Ascending compare-exchange of key[I], key[J] (static indices: stays in registers).
+#define BCHK_CAS(I, J)                                                  \
+    {                                                                   \
+        const uint32_t a_ = key[I], b_ = key[J];                        \
+        key[I] = a_ < b_ ? a_ : b_;                                     \
+        key[J] = a_ < b_ ? b_ : a_;                                     \
+    }
+
+// Bitonic sort of key[O .. O+16), ascending.
+template <int O>
+__device__ __forceinline__ void sort16(uint32_t *key) {
+#pragma unroll
+    for (int k = 2; k <= 16; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    if (i & k) BCHK_CAS(O + l, O + i) else BCHK_CAS(O + i, O + l)
+                }
+            }
+        }
+    }
+}
+
+// key[A..A+16) and key[B..B+16) sorted -> key[A..A+16) = the 16 smallest of both, sorted:
+// min(A_i, B_15-i) is bitonic, then a bitonic merge.
+template <int A, int B>
+__device__ __forceinline__ void merge_low16(uint32_t *key) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t a = key[A + i], b = key[B + 15 - i];
+        key[A + i] = a < b ? a : b;
+    }
+#pragma unroll
+    for (int j = 8; j > 0; j >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (!(i & j)) BCHK_CAS(A + i, A + i + j)
+    }
+}
 
 // 32-bit sort key: a monotone 26-bit prefix of |y| (5 exponent bits covering
 // [2^-27, 2^5) + 21 mantissa bits) above the 6-bit position. |y| below the range maps to
@@ -46,15 +90,19 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t hi, uint32_t lo, int pos) 
 // Blocks of kFastWaves waves, one 64-codeword chunk per wave: the code tables are staged
 // into LDS once per 512 codewords, and two blocks per CU give 4 waves per SIMD (<= 128
 // VGPRs; the kernel is latency-bound, so occupancy wins).
-template <int M, int TMAX>
+// SEL (no per-codeword stats requested, 2 TMAX + 2 <= 16): only the 16 smallest keys are
+// put in order (four sorted groups of 16, then low-half merges) -- the fast-path exits read
+// ranks 0..2t and the least reliable position, so an exact tie beyond rank 2t + 1 cannot
+// change a result, only the BCHK_F_TIE flag of the stats record; SEL = false sorts all 64
+// keys and sends any tie to the exact path, so the flags match it.
+template <int M, int TMAX, bool SEL>
 __global__ void __launch_bounds__(kWaveSize * kFastWaves, 4)
 kaneko_fast_kernel(SearchParams p) {
     constexpr int N = Geo<M>::N;
     static_assert(N <= 63, "fast path covers n <= 63");
     constexpr int W = (TMAX + 3) / 4;
     // calcRightSide takes the first border = 2t+1-m agreeing sorted positions; with m0 == m
-    // (both fast-path exits) and m positions disagreeing, they lie within ranks 0..2t.
-    constexpr int KMAX = (2 * TMAX < N - 1) ? 2 * TMAX : N - 1;
+    // (both fast-path exits) and m positions disagreeing, they lie within ranks 0..2t (KMAX).
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
     __syncthreads();
@@ -148,22 +196,43 @@ kaneko_fast_kernel(SearchParams p) {
     return;
 #endif
 
-    // ---- bitonic sort of the 64 keys, ascending
+    constexpr int KMAX = (2 * TMAX < N - 1) ? 2 * TMAX : N - 1;
+    static_assert(!SEL || KMAX + 2 <= 16, "selection keeps 16 ranks");
+    uint32_t kmax_real = 0;  // the largest key of a real position (SEL)
+    if constexpr (SEL) {
+        // ---- the 16 smallest keys in order: four sorted groups, low halves merged
+        sort16<0>(key);
+        sort16<16>(key);
+        sort16<32>(key);
+        sort16<48>(key);
+        // padding keys (positions >= N) are all-ones and sort to the top of their group
 #pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
+        for (int g = 0; g < 4; ++g) {
+            const int cnt = N - 16 * g < 0 ? 0 : (N - 16 * g > 16 ? 16 : N - 16 * g);
+            if (cnt > 0) kmax_real = key[16 * g + cnt - 1] > kmax_real ? key[16 * g + cnt - 1] : kmax_real;
+        }
+        merge_low16<0, 16>(key);
+        merge_low16<32, 48>(key);
+        merge_low16<0, 32>(key);
+    } else {
+        // ---- bitonic sort of the 64 keys, ascending
 #pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
-            for (int i = 0; i < 64; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const uint32_t a = key[i], b = key[l];
-                    const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-                    key[i] = (i & k) ? hi : lo;
-                    key[l] = (i & k) ? lo : hi;
+            for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+                for (int i = 0; i < 64; ++i) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const uint32_t a = key[i], b = key[l];
+                        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+                        key[i] = (i & k) ? hi : lo;
+                        key[l] = (i & k) ? lo : hi;
+                    }
                 }
             }
         }
+        kmax_real = key[N - 1];
     }
 
     BCHK_STAMP(1)
@@ -177,9 +246,10 @@ kaneko_fast_kernel(SearchParams p) {
     // path: beyond rank KMAX+1 the order cannot change this path's result, but an exact
     // tie anywhere is flagged (BCHK_F_TIE) there, so every path reports the same flags.
     bool bad = (key[0] >> 6) == 0u                       // some |y| < 2^-27 (or zero)
-               || (key[N - 1] >> 6) == 0x3FFFFFFu;       // some |y| >= 32, inf or NaN
+               || (kmax_real >> 6) == 0x3FFFFFFu;        // some |y| >= 32, inf or NaN
+    constexpr int NTIE = SEL ? KMAX + 1 : N - 1;         // adjacent pairs checked for ties
 #pragma unroll
-    for (int r = 0; r < N - 1; ++r) bad |= ((key[r] ^ key[r + 1]) >> 6) == 0u;
+    for (int r = 0; r < NTIE; ++r) bad |= ((key[r] ^ key[r + 1]) >> 6) == 0u;
     {   // materialise the flag here, so the sorted keys past the prefix die now
         uint32_t b = bad ? 1u : 0u;
         asm volatile("" : "+v"(b));
@@ -269,7 +339,11 @@ kaneko_fast_kernel(SearchParams p) {
     uint64_t best = 0;
     double l0 = DBL_MAX;
     Mask<1> E;
+#ifdef BCHK_FAST_VALU  // experiment: Berlekamp-Massey on the VALU (spread GF products)
+    const bool ok0 = alg_core_valu<M, TMAX>(chien, S0, t, E);
+#else
     const bool ok0 = alg_core<M, TMAX>(ex, lg, chien, S0, t, E);
+#endif
     if (!bad && ok0) {
         double l;
         bool ret;
@@ -299,7 +373,11 @@ kaneko_fast_kernel(SearchParams p) {
         uint32_t S1[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) S1[w] = S0[w] ^ col[o0 * W + w];
+#ifdef BCHK_FAST_VALU
+        const bool ok1 = alg_core_valu<M, TMAX>(chien, S1, t, E);
+#else
         const bool ok1 = alg_core<M, TMAX>(ex, lg, chien, S1, t, E);
+#endif
         if (need1 && ok1) {
             const uint64_t diff = (1ull << o0) ^ E.w[0];
             double l;
@@ -428,16 +506,27 @@ kaneko_fast_kernel(SearchParams p) {
     }
 }
 
-template <int M, int TMAX>
-static hipError_t launch_fast_impl(const SearchParams &p, size_t lds, hipStream_t s) {
+template <int M, int TMAX, bool SEL>
+static hipError_t launch_fast_sel(const SearchParams &p, size_t lds, hipStream_t s) {
     const uint32_t chunks = (p.count + 63u) / 64u;
     const int blocks = (int)((chunks + kFastWaves - 1) / kFastWaves);
     if (lds > 65536)
-        (void)hipFuncSetAttribute((const void *)&kaneko_fast_kernel<M, TMAX>,
+        (void)hipFuncSetAttribute((const void *)&kaneko_fast_kernel<M, TMAX, SEL>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((kaneko_fast_kernel<M, TMAX>), dim3(blocks), dim3(kWaveSize * kFastWaves),
+    hipLaunchKernelGGL((kaneko_fast_kernel<M, TMAX, SEL>), dim3(blocks), dim3(kWaveSize * kFastWaves),
                        lds, s, p);
     return hipGetLastError();
+}
+
+template <int M, int TMAX>
+static hipError_t launch_fast_impl(const SearchParams &p, size_t lds, hipStream_t s) {
+    constexpr int N = Geo<M>::N;
+    constexpr int KMAX = (2 * TMAX < N - 1) ? 2 * TMAX : N - 1;
+    if constexpr (KMAX + 2 <= 16) {
+        // no stats record: the flags are not observable, selection suffices
+        if (!p.st && !getenv("BCHK_FAST_FULLSORT")) return launch_fast_sel<M, TMAX, true>(p, lds, s);
+    }
+    return launch_fast_sel<M, TMAX, false>(p, lds, s);
 }
 
 size_t fast_wave_bytes() { return (size_t)kStageBytes; }

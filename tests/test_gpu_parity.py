@@ -473,3 +473,53 @@ def test_sub_batch_pipelines_match_one_pipeline(m, t, J, snr):
         outs.append((dres.cpu().numpy(), c6.cpu().numpy()))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("snr", [4.0, 5.0, 6.0])
+def test_fast_selection_equals_full_sort_with_far_ties(snr):
+    # Without a stats record the fast kernel orders only the 16 least reliable positions
+    # (kaneko_fast_kernel<.., SEL = true>); with one it sorts all 64 keys and sends every
+    # exact tie to the exact path. Rows with exact |y| ties among the reliable positions
+    # (beyond rank 2t + 1) must decode identically either way: words, l0 bits, counters.
+    import torch
+    d = dec(6, 6, J=15)
+    B = 1 << 16
+    tx, y, _ = d.generate(snr, B, seed=29)
+    y = y.copy()
+    rng = np.random.default_rng(5)
+    rows = rng.choice(B, B // 8, replace=False)
+    for r in rows:  # tie the two most reliable positions (and a far pair with opposite signs)
+        o = np.argsort(np.abs(y[r]))
+        y[r, o[-2]] = np.copysign(abs(y[r, o[-1]]), y[r, o[-2]])
+        y[r, o[-10]] = -y[r, o[-11]]
+    n = d.n
+    dy = torch.from_numpy(y).cuda()
+    dtx = torch.from_numpy(tx).cuda()
+    outs = []
+    for fused in (False, True):
+        dres = torch.zeros((B, n), dtype=torch.uint8, device="cuda")
+        dl0 = torch.zeros(B, dtype=torch.float64, device="cuda")
+        dst = torch.zeros((B, 56), dtype=torch.uint8, device="cuda")
+        c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        if fused:
+            d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), 0,
+                                  c6.data_ptr())
+        else:
+            d.decode_device(dy.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), dst.data_ptr())
+            d.count_device(dtx.data_ptr(), dres.data_ptr(), dst.data_ptr(), B, c6.data_ptr())
+        d.sync()
+        outs.append((dres.cpu().numpy(), dl0.cpu().numpy(), c6.cpu().numpy(), dst.cpu().numpy()))
+    (r0, l0a, c0, st0), (r1, l0b, c1, _) = outs
+    np.testing.assert_array_equal(r0, r1)
+    np.testing.assert_array_equal(l0a.view(np.uint64), l0b.view(np.uint64))
+    np.testing.assert_array_equal(c0, c1)
+    st = st0.view(load().STATS_DTYPE).reshape(B)
+    assert (st["flags"][rows] & load().F_TIE).all()  # the full sort saw the ties
+    # and the tied rows against the oracle
+    o = Oracle(6, 6)
+    idx = rows[:300]
+    r2, l2, s2, a2 = o.kaneko_batch(y[idx], J=15)
+    acc = a2.astype(bool)
+    np.testing.assert_array_equal(r1[idx][acc], r2[acc])
+    np.testing.assert_array_equal(l0b[idx][acc].view(np.uint64), l2[acc].view(np.uint64))
