@@ -194,6 +194,12 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
 
     def step():
         # everything below is enqueued on the decoder's stream (torch ops via ExternalStream)
+        if world == 1 and not args.unfused:
+            # one GPU: the fused call adds this step's counters straight into the totals
+            # (bchk_decode_count_device accumulates), no separate zero / add launches
+            dec.decode_count_device(d_y.data_ptr(), d_tx.data_ptr(), B, d_res.data_ptr(), d_l0.data_ptr(), 0,
+                                    d_cnt.data_ptr(), dec.stream)
+            return
         d_step.zero_()
         if args.unfused:  # decode, then the counters from a re-read of res / stats
             dec.decode_device(d_y.data_ptr(), B, d_res.data_ptr(), d_l0.data_ptr(), d_st.data_ptr(),
