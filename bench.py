@@ -237,11 +237,21 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
         torch.cuda.synchronize()
     ms4, launches = dec.profile_read_stages()  # fast, exact first pass, coop, analytic tail
     dec.profile(False)
+    # FER / op counters of the batch itself: every step re-decodes the same resident words,
+    # so the counts come from ONE more step on zeroed counters (world * B distinct words)
+    with torch.cuda.stream(stream):
+        dec.sync()
+        d_cnt.zero_()
+        dec.sync()
+        step()
+        dec.sync()
+        torch.cuda.synchronize()
     n_exact, n_coop = dec.path_counts()
     n_tail = dec.tail_count()
     tail_stats = dec.tail_stats()
     elapsed = max_over_ranks(elapsed, world, dist, dev)
-    cnt = d_cnt.cpu().numpy().astype(np.int64)  # summed over ranks (N > 1)
+    cnt = d_cnt.cpu().numpy().astype(np.int64)  # one pass over the batch, summed over ranks (N > 1)
+    assert int(cnt[5]) == world * B, "counters must cover every word of the batch once"
     total_words = world * B * args.steps
     value = total_words / elapsed
     # Algorithmic bytes per codeword: 8n B of f64 samples in, n B decoded bits and 8 B l0

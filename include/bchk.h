@@ -9,7 +9,15 @@
  *  - Every function returns 0 on success and a negative BCHK_E* code on failure;
  *    bchk_last_error() describes the last failure of the calling thread. Nothing throws.
  *  - One context = one (code, J, decoder SNR, device); it owns a HIP stream. A context
- *    is not thread-safe; use one per host thread.
+ *    is not thread-safe; use one per host thread. It also owns the work queues, control
+ *    words and fused-counter slots of its decode calls: at most ONE decode call per
+ *    context may be in flight on the device at a time. Calls enqueued on the same stream
+ *    serialise by themselves; a caller that passes different streams to consecutive calls
+ *    must order them (an event, or bchk_sync) -- otherwise one call's counter reduction
+ *    can fold and zero the other's partial counts. Use one context per concurrent stream.
+ *  - Kernels never hang on a work-queue wait: every wait is bounded, and a wait that runs
+ *    out leaves its codeword unfinished and sets the context's fault word. bchk_sync (and
+ *    every synchronous *_host call) then fails with BCHK_EHIP and clears it.
  *  - Bit vectors are one byte per position (0/1), position i = coefficient of x^i,
  *    exactly as the reference's unsigned char arrays.
  *  - *_host functions take host pointers and are synchronous. *_device functions take
@@ -159,7 +167,12 @@ int bchk_generate_device(bchk_ctx *ctx, double snr_db, size_t B, uint64_t seed, 
  * decode and counters fused (bchk_decode_count_device), Eb/N0 0..max_snr step 0.5, each point
  * until p words or e frame errors (the e-th error cut exactly in word order). CSV lines as
  * bchk_sweep (statistically the reference's, not byte-identical); seconds = wall time,
- * words = words decoded. */
+ * words = words decoded. One divergence in the BER column: a word the decoder never accepts
+ * is compared against the row left at its index in the batch buffer (zero in the first batch,
+ * else that row's last accepted word), whereas fun() compares it against the previous word's
+ * decision (its `decoded` buffer is shared, src/dataForPlot.cpp:25,52). FER, decodes,
+ * comparisons and sums are unaffected only when every word is accepted; unaccepted words are
+ * rare (none in the fixtures at n <= 63). bchk_sweep keeps fun()'s carry exactly. */
 int bchk_sweep_device(bchk_ctx *ctx, long p, long e, double max_snr, uint64_t seed, size_t batch,
                       char *csv, size_t cap, double *seconds, uint64_t *words);
 

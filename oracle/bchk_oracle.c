@@ -16,6 +16,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <pthread.h>
 
 static const unsigned kPrim[16] = {3, 7, 11, 19, 37, 67, 137, 285, 529, 1033,
                                    2053, 4179, 8219, 17475, 32771, 69643}; /* main.cpp:14 */
@@ -375,6 +376,60 @@ void orc_kaneko_decode(const orc_code *c, double s2, int J, const double *y,
     s.sum = s.iters * (uint64_t)(n + 1) + s.jsteps;
     if (l0_out) *l0_out = l0;
     if (st) *st = s;
+}
+
+/* ------------------------------------------------------ batch (threaded) */
+typedef struct {
+    const orc_code *c;
+    double s2;
+    int J;
+    const double *Y;
+    long B;
+    unsigned char *res, *acc;
+    double *l0;
+    uint64_t *st6;
+    long next; /* next unclaimed row (claimed in chunks under `mu`) */
+    pthread_mutex_t mu;
+} orc_batch_job;
+
+static void *orc_batch_worker(void *arg) {
+    orc_batch_job *j = (orc_batch_job *)arg;
+    const long n = j->c->n, chunk = 16;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        const long b0 = j->next;
+        j->next += chunk;
+        pthread_mutex_unlock(&j->mu);
+        if (b0 >= j->B) break;
+        const long b1 = b0 + chunk < j->B ? b0 + chunk : j->B;
+        for (long b = b0; b < b1; ++b) {
+            orc_stats s;
+            orc_kaneko_decode(j->c, j->s2, j->J, j->Y + b * n, j->res + b * n, &j->l0[b], &s);
+            uint64_t *o = j->st6 + 6 * b;
+            o[0] = s.decodes; o[1] = s.cmp; o[2] = s.sum;
+            o[3] = s.iters; o[4] = s.jsteps; o[5] = s.improvements;
+            j->acc[b] = (unsigned char)s.accepted;
+        }
+    }
+    return NULL;
+}
+
+void orc_kaneko_batch(const orc_code *c, double s2, int J, const double *Y, long B,
+                      unsigned char *res, double *l0, uint64_t *stats6, unsigned char *acc,
+                      int threads) {
+    enum { MAXTH = 256 };
+    if (threads < 1) threads = 1;
+    if (threads > MAXTH) threads = MAXTH;
+    pthread_t th[MAXTH];
+    int started[MAXTH] = {0};
+    /* rows are claimed dynamically: a heavy codeword (up to 2^31 - 1 test patterns) must not
+     * hold up a statically assigned range */
+    orc_batch_job job = {c, s2, J, Y, B, res, acc, l0, stats6, 0, PTHREAD_MUTEX_INITIALIZER};
+    for (int q = 1; q < threads; ++q)
+        started[q] = pthread_create(&th[q], NULL, orc_batch_worker, &job) == 0;
+    orc_batch_worker(&job);
+    for (int q = 1; q < threads; ++q)
+        if (started[q]) pthread_join(th[q], NULL);
 }
 
 /* ------------------------------------------------------------------- sweep */

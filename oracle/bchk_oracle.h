@@ -63,6 +63,14 @@ int orc_alg_decode_bm(const orc_code *c, const unsigned char *word, unsigned cha
 void orc_kaneko_decode(const orc_code *c, double s2, int J, const double *y,
                        unsigned char *res, double *l0, orc_stats *st);
 
+/* B independent decodes of the rows of Y [B][n] (orc_kaneko_decode each), split over
+ * `threads` POSIX threads (the oracle keeps no global state). res rows are written only on
+ * acceptance (callers pre-fill them); stats6 [B][6] = decodes, cmp, sum, iters, jsteps,
+ * improvements; acc [B] = accepted. Test infrastructure: the checker for full batches. */
+void orc_kaneko_batch(const orc_code *c, double s2, int J, const double *Y, long B,
+                      unsigned char *res, double *l0, uint64_t *stats6, unsigned char *acc,
+                      int threads);
+
 /* Monte-Carlo FER sweep fun(), src/dataForPlot.cpp:16-116, into a text buffer
  * (CSV). Returns the number of bytes written (or -1 if cap is too small). */
 /* Engine draws of `count` stream words from state *state (advanced), at Eb/N0 snr_db:

@@ -13,6 +13,9 @@ constexpr int kMaxT = 32;
 constexpr int kWaveSize = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
+// fault bits (SearchParams::fault)
+constexpr uint32_t kFaultHeavySlot = 1u, kFaultHeavyWait = 2u, kFaultTailSlot = 4u, kFaultTailWait = 8u,
+                   kFaultCoopRing = 16u;
 
 // Per-code lookup tables, one device blob, copied into LDS by every workgroup.
 //   exp8 [2n]        alpha^i for i < 2n-1, exp8[2n-1] = 0 (log sums are clamped to
@@ -118,6 +121,10 @@ struct SearchParams {
     unsigned long long *tail_diag;
     uint32_t *tail_diag_count;
     uint32_t tail_diag_cap;
+    // sticky per-context fault word (null = off): a bounded queue wait that ran out sets a
+    // bit (kFault*), since its codeword is then not finished; bchk_sync / the host decode
+    // calls report it as BCHK_EHIP and clear it
+    uint32_t *fault;
     // FER/BER/op counters fused into the decode (null = off): every kernel that finishes a
     // codeword compares its row with the sent word tx [B][n] and adds {frame errors, bit
     // errors, decodes, comparisons, sums, words} to the partial counters

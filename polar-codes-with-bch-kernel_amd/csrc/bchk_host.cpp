@@ -408,6 +408,7 @@ struct bchk_ctx {
     uint64_t tail_min_bound = 0;
     DevBuf tdiag;
     DevBuf cnt;  // fused FER/op counters: kCntSlots partial slots
+    DevBuf fault;  // sticky fault word (SearchParams::fault), checked by bchk_sync
     DevBuf gtx, gy, gres, gst, gcnt, gflags;  // bchk_sweep_device's batch buffers
     bool profile = false;
     // syndrome decoding table (bchk_syndtab.h): built on first use, shared across contexts
@@ -543,6 +544,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
     p.t = c->t;
     p.J = c->J;
     p.variant = variant;
+    p.fault = (uint32_t *)c->fault.p;
     if (d_tx) {  // fused counters (zeroed by launch_search at allocation, then by every reduction)
         p.tx = d_tx;
         p.cnt = (unsigned long long *)c->cnt.p;
@@ -797,7 +799,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (hipMalloc(&c->d_tables, c->td.bytes) != hipSuccess ||
         hipMemcpy(c->d_tables, c->tables_host.data(), c->td.bytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        ensure_pipes(c, 1) != 0) {
+        ensure_pipes(c, 1) != 0 || c->fault.ensure(128) != 0 ||
+        hipMemset(c->fault.p, 0, 128) != hipSuccess) {
         bchk_destroy(c);
         return fail(BCHK_EHIP, "device setup failed: %s", hipGetErrorString(hipGetLastError()));
     }
@@ -857,6 +860,8 @@ void bchk_destroy(bchk_ctx *c) {
     release_pipes(c);
     c->tdiag.release();
     c->cnt.release();
+    c->fault.release();
+    c->diag.release();
     for (DevBuf *b : {&c->gtx, &c->gy, &c->gres, &c->gst, &c->gcnt, &c->gflags}) b->release();
     c->y.release();
     c->res.release();
@@ -892,10 +897,24 @@ int bchk_set_max_decodes(bchk_ctx *c, uint64_t md) {
 
 void *bchk_stream(bchk_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
+// After the context's stream has drained: a bounded queue wait that ran out in a kernel
+// (SearchParams::fault) means codewords were left unfinished -- an error, cleared once read.
+static int check_fault(bchk_ctx *c) {
+    if (!c->fault.p) return 0;
+    uint32_t f = 0;
+    HIP_TRY(hipMemcpyAsync(&f, c->fault.p, sizeof f, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!f) return 0;
+    HIP_TRY(hipMemsetAsync(c->fault.p, 0, sizeof f, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return fail(BCHK_EHIP, "a work-queue wait timed out in a decode kernel (fault bits %#x): codewords "
+                "were left unfinished", f);
+}
+
 int bchk_sync(bchk_ctx *c) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return 0;
+    return check_fault(c);
 }
 
 int bchk_decode_device(bchk_ctx *c, const double *d_y, size_t B, uint8_t *d_res, double *d_l0,
@@ -926,7 +945,7 @@ int bchk_decode_variant_host(bchk_ctx *c, int variant, const double *y, size_t B
     if (l0) HIP_TRY(hipMemcpyAsync(l0, c->l0.p, B * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     if (st) HIP_TRY(hipMemcpyAsync(st, c->st.p, B * sizeof(bchk_stats), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return 0;
+    return check_fault(c);
 }
 
 int bchk_decode_host(bchk_ctx *c, const double *y, size_t B, uint8_t *res, double *l0, bchk_stats *st) {
@@ -1171,6 +1190,9 @@ int bchk_sweep_device(bchk_ctx *c, long p, long e, double max_snr, uint64_t seed
                 return rc;
             HIP_TRY(hipMemcpyAsync(h, d6, sizeof h, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
+            if ((rc = check_fault(c))) return rc;
+            if (h[5] != nb)  // every word of the batch must have been finished and counted
+                return fail(BCHK_EHIP, "fused counters saw %llu of %zu words", (unsigned long long)h[5], nb);
             decoded += nb;
             size_t used = nb;
             if (countErr + (long)h[0] >= e) {  // the e-th error falls in this batch: cut there

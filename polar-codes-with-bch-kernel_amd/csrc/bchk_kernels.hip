@@ -1406,6 +1406,11 @@ __device__ __forceinline__ void wave_done(const SearchParams &p, int lane, uint3
 // tail, then stores the codeword; consumers restore empty slots), kEmptySlot once the
 // first pass has finished (its per-XCD done counts reach *in_total) and no ticket is left.
 // Every wait is bounded (a logic error ends the wave instead of hanging it).
+// A bounded wait ran out (a logic error: its codeword stays unfinished): tell the host.
+__device__ __forceinline__ void flag_fault(const SearchParams &p, uint32_t bit) {
+    if (p.fault) atomicOr(p.fault, bit);
+}
+
 __device__ uint32_t tail_dequeue(const SearchParams &p, uint32_t &item) {
     constexpr uint32_t kTailSpin = 1u << 24;  // ~1 s of polling: a guard against logic errors
     const uint32_t total = p.in_total ? *p.in_total : p.count;
@@ -1422,6 +1427,7 @@ __device__ uint32_t tail_dequeue(const SearchParams &p, uint32_t &item) {
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
+            flag_fault(p, kFaultTailSlot);
             return kEmptySlot;
         }
         uint32_t done = 0;
@@ -1433,6 +1439,7 @@ __device__ uint32_t tail_dequeue(const SearchParams &p, uint32_t &item) {
         if (final) return kEmptySlot;
         __builtin_amdgcn_s_sleep(16);
     }
+    flag_fault(p, kFaultTailWait);
     return kEmptySlot;
 }
 
@@ -1644,16 +1651,17 @@ __device__ uint32_t next_heavy(const SearchParams &p) {
         uint32_t *head = q ? p.heavy_head2 : p.heavy_head;
         const uint32_t *tail = q ? p.heavy_tail2 : p.heavy_tail;
         const uint32_t k = atomicAdd(head, 1u);
-        bool have = false;
+        bool have = false, final = false;
         for (uint32_t spins = 0; spins < kSpinLimit; ++spins) {
             if (k < ld_rlx(tail)) { have = true; break; }
             // the counts first (and waited for): if complete, the tail read after is final
-            const bool final = exact_finished(p) >= total;
+            final = exact_finished(p) >= total;
             mem_drain();
             if (k < ld_rlx(tail)) { have = true; break; }
             if (final) break;
             __builtin_amdgcn_s_sleep(32);
         }
+        if (!have && !final) flag_fault(p, kFaultHeavyWait);
         if (!have) continue;
         uint32_t *slot = q ? p.heavy_queue + (p.count - 1u - k) : p.heavy_queue + k;
         for (uint32_t w = 0; w < kSpinLimit; ++w) {  // the producer stores after reserving
@@ -1664,6 +1672,7 @@ __device__ uint32_t next_heavy(const SearchParams &p) {
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        flag_fault(p, kFaultHeavySlot);
         return kEmptySlot;
     }
     return kEmptySlot;
@@ -1835,6 +1844,7 @@ kaneko_coop_kernel(SearchParams p) {
                 const int run = (int)__builtin_ctzll(~rm);  // chunks c .. c + run - 1 ready
                 if (run == 0) {
                     if (++spins > kSpinLimit) {  // never expected: fail the codeword, no hang
+                        if (lane == 0) flag_fault(p, kFaultCoopRing);
                         S.i_end = 64ull * c;
                         S.truncated = true;
                         break;

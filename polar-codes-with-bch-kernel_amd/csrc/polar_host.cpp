@@ -249,7 +249,7 @@ int build_trellis(const uint32_t *rows, int l, std::vector<uint32_t> &ent, uint3
             }
             cw0.swap(cw1);
             if (end[j] != ~0u) {
-                memmove(active + B, active + B + 1, sizeof(unsigned) * (na - B));
+                memmove(active + B, active + B + 1, sizeof(unsigned) * (na - B - 1));
                 --na;
             }
             if (na != na1) return pfail(BCHK_EINVAL, "trellis construction inconsistent"), 0;

@@ -30,6 +30,14 @@ class OrcStats(C.Structure):
 _lib = None
 
 
+def host_threads():
+    """Checker threads: this process's CPU affinity, capped by the job share a GPU box
+    exports (OMP_NUM_THREADS; os.cpu_count() there is the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(share))) if share.isdigit() and int(share) > 0 else max(1, n)
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -43,6 +51,8 @@ def lib():
         L.orc_alg_decode_bm.argtypes = [P(OrcCode), C.c_void_p, C.c_void_p]
         L.orc_kaneko_decode.argtypes = [P(OrcCode), C.c_double, C.c_int, C.c_void_p,
                                         C.c_void_p, P(C.c_double), P(OrcStats)]
+        L.orc_kaneko_batch.argtypes = [P(OrcCode), C.c_double, C.c_int, C.c_void_p, C.c_long,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_sweep.argtypes = [P(OrcCode), C.c_double, C.c_int, C.c_long, C.c_long,
                                 C.c_double, C.c_uint64, C.c_char_p, C.c_long]
         L.orc_sweep.restype = C.c_long
@@ -99,18 +109,19 @@ class Oracle:
                                 _p(y), _p(res), C.byref(l0), C.byref(st))
         return res, l0.value, st
 
-    def kaneko_batch(self, Y, J=-1):
+    def kaneko_batch(self, Y, J=-1, threads=None):
+        """Rows of Y decoded independently (orc_kaneko_batch, POSIX threads): res (0xFF rows
+        where nothing was accepted), l0, stats [B][6] (decodes, cmp, sum, iters, jsteps,
+        improvements), accepted."""
+        Y = np.ascontiguousarray(Y, np.float64)
         B = Y.shape[0]
         res = np.full((B, self.n), 0xFF, np.uint8)
         l0 = np.zeros(B)
         stats = np.zeros((B, 6), np.uint64)
         acc = np.zeros(B, np.uint8)
-        s2 = self.s2()
-        for b in range(B):
-            r, l, st = self.kaneko(Y[b], J, s2)
-            res[b], l0[b] = r, l
-            stats[b] = (st.decodes, st.cmp, st.sum, st.iters, st.jsteps, st.improvements)
-            acc[b] = st.accepted
+        if B:
+            lib().orc_kaneko_batch(C.byref(self.code), self.s2(), J, _p(Y), B, _p(res), _p(l0),
+                                   _p(stats), _p(acc), threads or host_threads())
         return res, l0, stats, acc
 
     def sweep(self, p, e, J=-1, max_snr=5.0, seed=1, decoder_snr_db=0.5):
