@@ -139,13 +139,34 @@ int bchk_generate_host_draws(const bchk_ctx *ctx, double snr_db, size_t B, uint6
  * process. */
 uint64_t bchk_rng_jump(uint64_t state, uint64_t draws);
 /* One block of a (sharded) fun() sweep (src/dataForPlot.cpp:41-74): from engine state
- * *rng_state (in/out), `skip` words are generated and dropped (the blocks of other ranks),
+ * *rng_state (in/out), `skip` words are passed over (their engine draws only, no samples),
  * then B words are generated at Eb/N0 snr_db and decoded on the GPU:
  *   tx [B][n], res [B][n] (zero where not accepted), accepted [B], ops [B][3] = decodes,
  *   comparisons, sums, states [B] = engine state after word b (where a sweep resumes when
  *   it stops after word b). */
 int bchk_sweep_block(bchk_ctx *ctx, double snr_db, uint64_t *rng_state, size_t skip, size_t B,
                      uint8_t *tx, uint8_t *res, uint8_t *accepted, uint64_t *ops, uint64_t *states);
+/* The same over the words of a stretch of the stream given in engine draws: from *rng_state
+ * (a word start; in/out) words are generated until exactly `draws` draws are consumed (an
+ * error if the stretch does not end on a word boundary or holds more than max_words words);
+ * *words = their count. A sharded sweep's rank decodes the stretch between two word starts
+ * found by bchk_stream_sync. */
+int bchk_sweep_range(bchk_ctx *ctx, double snr_db, uint64_t *rng_state, uint64_t draws, size_t max_words,
+                     uint8_t *tx, uint8_t *res, uint8_t *accepted, uint64_t *ops, uint64_t *states,
+                     size_t *words);
+/* The reference stream's draw structure for a code of dimension k and length n (host only,
+ * no device): a word is k information draws (uniform_int_distribution<unsigned short>(0, 1),
+ * src/bchCoder.cpp:236-240, redrawn only for the two largest engine values) and polar-method
+ * attempts of four draws until ceil(n/2) pairs are accepted (normal_distribution, :243-250).
+ * bchk_stream_skip: the engine state and draws after `words` words from `state` (no samples).
+ * bchk_stream_sync: from a word start `state`, the first word start at or after `offset` draws
+ * on the stream's own parse, found WITHOUT parsing the draws before `offset` (every parse
+ * state possible at `offset` is followed until they merge; a redrawn information bit before
+ * `offset`, or no merge before offset + limit, returns 1 = unresolved): *word_offset (draws
+ * from `state`) and *word_state. */
+int bchk_stream_skip(int k, int n, uint64_t state, uint64_t words, uint64_t *state_out, uint64_t *draws);
+int bchk_stream_sync(int k, int n, uint64_t state, uint64_t offset, uint64_t limit, uint64_t *word_offset,
+                     uint64_t *word_state);
 
 /* fun(file, decoder, g, gSize, p, e, maxSTNR) (headers/dataForPlot.h:8,
  * src/dataForPlot.cpp:16-116) on the GPU: identical CSV text, written to csv (cap bytes,
@@ -238,8 +259,11 @@ typedef struct bchk_polar bchk_polar;
  * specification (out/external/MixedKernelEncoder.cpp:7-98: "N K d layers #shortened
  * #punctured", kernel names, shortened / punctured symbols, U - K freezing constraints).
  * Kernels: Arikan ("A") layers, and matrix kernels ("-file" / "<file", a size and size^2
- * entries, Kernel.cpp:93-107 -- e.g. BCH-derived kernels) of size <= 16, whose kernel LLRs are
- * the trellis min-sum of out/external/TrellisKernelProcessor.cpp:234-294 (polar_mixed.hip);
+ * entries, Kernel.cpp:93-107 -- e.g. BCH-derived kernels) of size <= 64, whose kernel LLRs are
+ * the trellis min-sum of out/external/TrellisKernelProcessor.cpp:234-294 (polar_mixed.hip):
+ * coset enumeration below 16, the trellis for 16..32 (at most 2^12 states per depth), and an
+ * exact ordered-statistics search above 32 (the 64 x 64 extended-BCH kernel; the reference's
+ * trellis processor stops below 64) -- the same value bit for bit;
  * 1 <= list_size <= 32, lengths whose per-wave state fits the 160 KiB LDS (U <= 1024 at
  * L = 16, 2048 at L = 8 for all-Arikan codes). Kernel files are read relative to kdir. */
 int bchk_polar_create(const char *spec, int list_size, int device, bchk_polar **out);
@@ -265,7 +289,7 @@ void *bchk_polar_stream(bchk_polar *pc);
 /* ---- BCH polar-kernel construction and the column-permutation search (root bchCoder.cpp;
  * csrc/kernel_search.hip). Kernels are row-major l x l bytes (0/1). */
 /* makeMatrix (root bchCoder.cpp:356-389): the nested extended-BCH kernel of size 2^power
- * (2 <= power <= 5), GF(2^power) from the reference's primitive polynomials
+ * (2 <= power <= 6), GF(2^power) from the reference's primitive polynomials
  * (src/main.cpp:14-15). Columns in power order: column 0 the extension, column p + 1 the
  * position of alpha^p. */
 int bchk_kernel_ebch(int power, uint8_t *K);

@@ -525,3 +525,43 @@ void orc_sweep_block(const orc_code *c, double decoder_snr_db, int J, double snr
     }
     *state = r.x;
 }
+
+/* fun()'s loop body over the words of a stretch of `draws` engine draws from word start *state
+ * (advanced): words generated one by one (their draws counted by stepping a copy of the
+ * engine, as orc_stream_draws) until exactly `draws` are consumed. Returns the word count,
+ * -1 if the stretch does not end on a word boundary or holds more than max_words words. */
+long orc_sweep_range(const orc_code *c, double decoder_snr_db, int J, double snr_db, uint64_t *state,
+                     uint64_t draws, long max_words, unsigned char *tx, unsigned char *res, unsigned char *acc,
+                     uint64_t *ops, uint64_t *states) {
+    orc_rng r = {*state}, probe;
+    unsigned char info[ORC_MAXN + 1];
+    double y[ORC_MAXN + 1];
+    const double sd = orc_sigma(c, snr_db), s2 = pow(orc_sigma(c, decoder_snr_db), 2);
+    const int n = c->n;
+    uint64_t used = 0;
+    long b = 0;
+    while (used < draws) {
+        if (b >= max_words) return -1;
+        probe = r;
+        orc_gen_info(&r, info, c->k);            /* dataForPlot.cpp:47-50 */
+        orc_encode(c, info, tx + b * n);
+        orc_add_noise(&r, sd, tx + b * n, y, n);
+        while (probe.x != r.x) {
+            probe.x = (probe.x * 16807u) % 2147483647u;
+            ++used;
+        }
+        orc_stats st;
+        memset(res + b * n, 0, (size_t)n);
+        orc_kaneko_decode(c, s2, J, y, res + b * n, NULL, &st);  /* :52 */
+        acc[b] = (unsigned char)st.accepted;
+        ops[3 * b] = st.decodes;
+        ops[3 * b + 1] = st.cmp;
+        ops[3 * b + 2] = st.sum;
+        states[b] = r.x;
+        ++b;
+    }
+    if (used != draws) return -1;
+    *state = r.x;
+    return b;
+}
+

@@ -83,6 +83,9 @@ uint64_t orc_stream_draws(const orc_code *c, uint64_t *state, long count, double
 void orc_sweep_block(const orc_code *c, double decoder_snr_db, int J, double snr_db, uint64_t *state,
                      long skip, long B, unsigned char *tx, unsigned char *res, unsigned char *acc,
                      uint64_t *ops, uint64_t *states);
+long orc_sweep_range(const orc_code *c, double decoder_snr_db, int J, double snr_db, uint64_t *state,
+                     uint64_t draws, long max_words, unsigned char *tx, unsigned char *res, unsigned char *acc,
+                     uint64_t *ops, uint64_t *states);
 long orc_sweep(const orc_code *c, double decoder_snr_db, int J, long p, long e,
                double max_snr, uint64_t seed, char *out, long cap);
 

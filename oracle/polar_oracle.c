@@ -332,15 +332,17 @@ static void arikan_llr(int phase, int d, const uint8_t *known, const float *src,
  * construction (TrellisKernelProcessor.cpp:69-179, MinimumSpan :7-67) and walk (:260-292)
  * state by state, float metrics. Same value as the enumeration (min commutes with the
  * monotone float add along each word's left-to-right sum). */
+typedef unsigned __int128 u128; /* kernel rows plus the extension column (size <= 64) */
+
 static float trellis_minsum_llr(const plr_kernel *k, int phase, const float *y) {
     const unsigned l = (unsigned)k->size, N = l + 1, K = l - (unsigned)phase;
-    uint64_t M[PLR_MAXKERNEL] = {0};
+    u128 M[PLR_MAXKERNEL] = {0};
     for (unsigned i = 0; i < K; ++i) {
         M[i] = 0;
         for (unsigned j = 0; j < l; ++j)
-            if (k->K[(phase + i) * l + j]) M[i] |= 1ull << j;
+            if (k->K[(phase + i) * l + j]) M[i] |= (u128)1 << j;
     }
-    M[0] |= 1ull << l;
+    M[0] |= (u128)1 << l;
     unsigned start[PLR_MAXKERNEL + 1], end[PLR_MAXKERNEL + 1], C = 0;
     for (unsigned c = 0; c < N; ++c) start[c] = end[c] = ~0u;
     for (unsigned i = 0; i < K; ++i) {
@@ -380,6 +382,7 @@ static float trellis_minsum_llr(const plr_kernel *k, int phase, const float *y) 
         a += (start[j] != ~0u) - (end[j] != ~0u);
     }
     const size_t cap = (size_t)1 << (most + 1);
+    /* labels are read at positions < l only: a state's word fits 64 bits without the extension */
     uint64_t *cw0 = calloc(cap, 8), *cw1 = calloc(cap, 8);
     float *m0 = malloc(cap * 4), *m1 = malloc(cap * 4);
     unsigned active[PLR_MAXKERNEL + 1], na = 0;
@@ -394,6 +397,7 @@ static float trellis_minsum_llr(const plr_kernel *k, int phase, const float *y) 
         for (uint64_t S = 0; S < (1ull << na1); ++S) m1[S] = INFINITY;
         const float Y = y[j], aY = fabsf(Y);
         const unsigned HD = Y < 0;
+        const uint64_t rowj = start[j] == ~0u ? 0 : (uint64_t)M[start[j]];
         for (uint64_t S = 0; S < ns; ++S) {
             uint64_t nx[2];
             uint64_t lab[2];
@@ -407,7 +411,7 @@ static float trellis_minsum_llr(const plr_kernel *k, int phase, const float *y) 
                 uint64_t n0 = S, n1 = S ^ (1ull << na);
                 nx[0] = (n0 & emask) | ((n0 >> 1) & ~emask);
                 nx[1] = (n1 & emask) | ((n1 >> 1) & ~emask);
-                const uint64_t c1 = cw0[S] ^ M[start[j]];
+                const uint64_t c1 = cw0[S] ^ rowj;
                 cw1[nx[0]] = cw0[S];
                 cw1[nx[1]] = c1;
                 lab[0] = (cw0[S] >> j) & 1;
@@ -421,7 +425,7 @@ static float trellis_minsum_llr(const plr_kernel *k, int phase, const float *y) 
         }
         if (start[j] != ~0u) active[na++] = start[j];
         if (end[j] != ~0u) {
-            memmove(active + B, active + B + 1, sizeof(unsigned) * (na - B));
+            memmove(active + B, active + B + 1, sizeof(unsigned) * (na - B - 1));
             --na;
         }
         { uint64_t *t = cw0; cw0 = cw1; cw1 = t; }
@@ -432,36 +436,137 @@ static float trellis_minsum_llr(const plr_kernel *k, int phase, const float *y) 
     return r;
 }
 
-/* cosets of more than 2^plr_trellis_nfree words go through the trellis (tests set it to
- * compare the two) */
-int plr_trellis_nfree = 12;
+/* metric of a word: the left-to-right float sum of |y| over its disagreeing positions
+ * (TrellisKernelProcessor.cpp:279-282 along one path) */
+static float word_metric(uint64_t dis, const float *ay, int l) {
+    float m = 0.0f;
+    for (int j = 0; j < l; ++j)
+        if ((dis >> j) & 1) m += ay[j];
+    return m;
+}
 
-float plr_minsum_llr(const plr_kernel *k, int phase, const float *y) {
-    const int l = k->size, nfree = l - phase - 1;
-    if (nfree > plr_trellis_nfree) return trellis_minsum_llr(k, phase, y);
-    uint32_t rows[PLR_MAXKERNEL];
+static void kernel_rows(const plr_kernel *k, uint64_t *rows) {
+    const int l = k->size;
     for (int r = 0; r < l; ++r) {
         rows[r] = 0;
         for (int j = 0; j < l; ++j)
-            if (k->K[r * l + j]) rows[r] |= 1u << j;
+            if (k->K[r * l + j]) rows[r] |= 1ull << j;
     }
-    uint32_t hd = 0;
-    for (int j = 0; j < l; ++j)
-        if (y[j] < 0) hd |= 1u << j; /* HD = Y < 0 (TrellisKernelProcessor.cpp:276) */
+}
+
+/* the coset enumerated: every word of rows phase+1..l-1 (Gray order, one row per step) */
+static float enum_minsum_llr(const plr_kernel *k, int phase, const float *y) {
+    const int l = k->size, nfree = l - phase - 1;
+    uint64_t rows[PLR_MAXKERNEL], hd = 0;
+    float ay[PLR_MAXKERNEL];
+    kernel_rows(k, rows);
+    for (int j = 0; j < l; ++j) {
+        if (y[j] < 0) hd |= 1ull << j; /* HD = Y < 0 (TrellisKernelProcessor.cpp:276) */
+        ay[j] = fabsf(y[j]);
+    }
     float best[2] = {INFINITY, INFINITY};
+    uint64_t c = 0;
     for (uint64_t v = 0; v < (1ull << nfree); ++v) {
-        uint32_t c = 0;
-        for (int r = 0; r < nfree; ++r)
-            if ((v >> r) & 1) c ^= rows[phase + 1 + r];
+        if (v) c ^= rows[phase + 1 + __builtin_ctzll(v)];
         for (int b = 0; b < 2; ++b) {
-            const uint32_t dis = (b ? c ^ rows[phase] : c) ^ hd;
-            float m = 0.0f; /* left-to-right sum, :279-282 */
-            for (int j = 0; j < l; ++j)
-                if ((dis >> j) & 1) m += fabsf(y[j]);
+            const float m = word_metric((b ? c ^ rows[phase] : c) ^ hd, ay, l);
             if (m < best[b]) best[b] = m;
         }
     }
     return best[1] - best[0]; /* :292 */
+}
+
+/* Exact ordered-statistics search, each half b of the coset on its own: Gauss-Jordan on rows
+ * phase+1..l-1 over the positions in decreasing |y| gives the most reliable basis (pivots); a
+ * word of half b is fixed by its pivot values, and the one matching the hard decision there
+ * is the root. Flipping a set E of pivots costs at least the sum of their |y| (they then
+ * disagree), so a depth-first search over E, cheapest pivot first, pruning every subtree whose
+ * flip cost exceeds the best metric found (less a float-rounding margin), visits every word
+ * that can be the minimum: the value is the enumeration's. */
+static __thread long ml_nodes_last;
+long plr_ml_nodes(void) { return ml_nodes_last; }
+
+static float ml_minsum_llr(const plr_kernel *k, int phase, const float *y) {
+    const int l = k->size, nf = l - phase - 1;
+    uint64_t rows[PLR_MAXKERNEL], G[PLR_MAXKERNEL], hd = 0;
+    float ay[PLR_MAXKERNEL];
+    int piv[PLR_MAXKERNEL], used[PLR_MAXKERNEL] = {0}, ord[PLR_MAXKERNEL], po[PLR_MAXKERNEL];
+    kernel_rows(k, rows);
+    for (int j = 0; j < l; ++j) {
+        if (y[j] < 0) hd |= 1ull << j;
+        ay[j] = fabsf(y[j]);
+        ord[j] = j;
+    }
+    for (int i = 1; i < l; ++i) { /* positions by decreasing |y| (insertion sort) */
+        const int p = ord[i];
+        int j = i - 1;
+        while (j >= 0 && ay[ord[j]] < ay[p]) { ord[j + 1] = ord[j]; --j; }
+        ord[j + 1] = p;
+    }
+    for (int i = 0; i < nf; ++i) G[i] = rows[phase + 1 + i];
+    int np = 0;
+    for (int s = 0; s < l && np < nf; ++s) {
+        const int p = ord[s];
+        int r = -1;
+        for (int i = 0; i < nf; ++i)
+            if (!used[i] && ((G[i] >> p) & 1)) { r = i; break; }
+        if (r < 0) continue;
+        used[r] = 1;
+        piv[r] = p;
+        po[nf - 1 - np] = r; /* found in decreasing |y|: po runs by increasing flip cost */
+        ++np;
+        for (int i = 0; i < nf; ++i)
+            if (i != r && ((G[i] >> p) & 1)) G[i] ^= G[r];
+    }
+    /* a float sum of at most 64 non-negative terms is within 64 u (u = 2^-24) of the exact
+     * sum: a subtree is pruned only when its exact cost exceeds best by more than that */
+    const double shrink = 1.0 - 1.0 / 32768.0;
+    float best[2];
+    typedef struct { uint64_t c; double lb; int i; } node;
+    node *st = malloc(sizeof(node) * (size_t)(nf + 2));
+    long nodes = 0;
+    for (int b = 0; b < 2; ++b) {
+        const uint64_t base = b ? rows[phase] : 0, target = hd ^ base;
+        uint64_t c = base;
+        for (int i = 0; i < nf; ++i)
+            if ((target >> piv[i]) & 1) c ^= G[i];
+        best[b] = word_metric(c ^ hd, ay, l);
+        ++nodes;
+        int sp = 0;
+        if (nf > 0) st[sp++] = (node){c, 0.0, 0};
+        while (sp) { /* (c, lb, i): the words c ^ G[po[j]] for j = i, i+1, ... and below them */
+            const node n = st[--sp];
+            for (int i = n.i; i < nf; ++i) {
+                const double lb2 = n.lb + ay[piv[po[i]]];
+                if (lb2 * shrink > best[b]) break; /* costs increase with i */
+                const uint64_t c2 = n.c ^ G[po[i]];
+                const float m = word_metric(c2 ^ hd, ay, l);
+                ++nodes;
+                if (m < best[b]) best[b] = m;
+                if (i + 1 < nf) st[sp++] = (node){c2, lb2, i + 1};
+            }
+        }
+    }
+    free(st);
+    ml_nodes_last = nodes;
+    return best[1] - best[0]; /* :292 */
+}
+
+/* cosets of more than 2^plr_trellis_nfree words go through the trellis (tests set it to
+ * compare the two) when the kernel has at most 32 rows, else through the ordered-statistics
+ * search (the reference's trellis processor takes kernels below 64 only) */
+int plr_trellis_nfree = 12;
+
+float plr_minsum_llr_by(const plr_kernel *k, int phase, const float *y, int method) {
+    if (method == PLR_BY_ENUM) return enum_minsum_llr(k, phase, y);
+    if (method == PLR_BY_TRELLIS) return trellis_minsum_llr(k, phase, y);
+    return ml_minsum_llr(k, phase, y);
+}
+
+float plr_minsum_llr(const plr_kernel *k, int phase, const float *y) {
+    const int l = k->size, nfree = l - phase - 1;
+    if (nfree <= plr_trellis_nfree) return enum_minsum_llr(k, phase, y);
+    return l <= 32 ? trellis_minsum_llr(k, phase, y) : ml_minsum_llr(k, phase, y);
 }
 
 /* CTrellisKernelProcessor::GetLLRs (:234-294): the offset state accumulates the known

@@ -9,7 +9,7 @@
 
 #define PLR_MAXLAYERS 16
 #define PLR_MAXU 4096
-#define PLR_MAXKERNEL 32 /* matrix kernels: min-sum by enumeration of 2^(size-1-phase) words */
+#define PLR_MAXKERNEL 64 /* matrix kernels up to 64 x 64 (the 2^6 extended-BCH kernel) */
 
 typedef struct {
     int size;
@@ -46,8 +46,22 @@ void plr_extract_info(const plr_code *P, const uint8_t *ucw, uint8_t *info);
  * codewords [L][N] (may be NULL), path metrics [L] (may be NULL). Returns count or <0. */
 int plr_decode(const plr_code *P, int L, const float *llr, uint8_t *info, uint8_t *cw,
                float *metric);
-/* one kernel-input LLR of a matrix kernel by exhaustive min-sum (exposed for tests):
- * y = the kernel's output LLRs with the known inputs' signs already applied */
+/* one kernel-input LLR of a matrix kernel: the min-sum value of CTrellisKernelProcessor::GetLLRs
+ * (out/external/TrellisKernelProcessor.cpp:234-294), best[1] - best[0] over the coset of rows
+ * phase+1..size-1, each word's metric the left-to-right float sum of |y| where it differs
+ * from the hard decision. y = the kernel's output LLRs with the known inputs' signs applied.
+ * Method: coset enumeration for cosets of at most 2^plr_trellis_nfree words; above that the
+ * literal trellis for sizes <= 32 and the exact ordered-statistics search for larger kernels
+ * (the reference's trellis processor stops below 64, TrellisKernelProcessor.cpp:70-71). */
 float plr_minsum_llr(const plr_kernel *k, int phase, const float *y);
+/* The same value by a given method (tests): PLR_BY_ENUM (2^(size-1-phase) words),
+ * PLR_BY_TRELLIS (the trellis, any size <= 64: 65 columns with the extension), PLR_BY_ML
+ * (exact ordered-statistics search with a lower-bound certificate). */
+#define PLR_BY_ENUM 0
+#define PLR_BY_TRELLIS 1
+#define PLR_BY_ML 2
+float plr_minsum_llr_by(const plr_kernel *k, int phase, const float *y, int method);
+/* nodes (candidate codewords) the last PLR_BY_ML call of this thread evaluated */
+long plr_ml_nodes(void);
 
 #endif

@@ -31,7 +31,8 @@ EXPORTS = (
     "bchk_create", "bchk_destroy", "bchk_code_params", "bchk_generator",
     "bchk_set_max_decodes", "bchk_decode_host", "bchk_decode_device",
     "bchk_decode_variant_host", "bchk_alg_decode_host", "bchk_count_device", "bchk_decode_count_device",
-    "bchk_generate_host", "bchk_generate_host_draws", "bchk_generate_device", "bchk_sweep_device", "bchk_rng_jump", "bchk_sweep_block", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
+    "bchk_generate_host", "bchk_generate_host_draws", "bchk_generate_device", "bchk_sweep_device", "bchk_rng_jump", "bchk_sweep_block", "bchk_sweep_range", "bchk_stream_skip",
+    "bchk_stream_sync", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
     "bchk_profile_read", "bchk_profile_read_stages", "bchk_path_counts", "bchk_tail_count",
     "bchk_tail_stats", "bchk_tail_diag_read", "bchk_set_fast_path", "bchk_set_analytic",
     "bchk_set_chunk_limit", "bchk_set_syndrome_table",
@@ -97,6 +98,9 @@ def lib():
     L.bchk_rng_jump.argtypes = [u64, u64]
     L.bchk_rng_jump.restype = u64
     L.bchk_sweep_block.argtypes = [vp, dbl, C.POINTER(u64), sz, sz, vp, vp, vp, vp, vp]
+    L.bchk_sweep_range.argtypes = [vp, dbl, C.POINTER(u64), u64, sz, vp, vp, vp, vp, vp, C.POINTER(sz)]
+    L.bchk_stream_skip.argtypes = [i32, i32, u64, u64, C.POINTER(u64), C.POINTER(u64)]
+    L.bchk_stream_sync.argtypes = [i32, i32, u64, u64, u64, C.POINTER(u64), C.POINTER(u64)]
     L.bchk_sweep.argtypes = [vp, C.c_long, C.c_long, dbl, C.POINTER(u64), u64, sz, C.c_char_p, sz]
     L.bchk_sync.argtypes = [vp]
     L.bchk_stream.argtypes = [vp]
@@ -254,6 +258,20 @@ class KanekoKernelProcessor:
                                       _p(ops), _p(states)))
         return tx, res, acc, ops, states, st.value
 
+    def sweep_range(self, snr_db, state, draws, max_words):
+        """The words of `draws` engine draws from word start `state` (bchk_sweep_range), as
+        sweep_block: (tx, res, accepted, ops, states, state after)."""
+        tx = np.zeros((max_words, self.n), np.uint8)
+        res = np.zeros((max_words, self.n), np.uint8)
+        acc = np.zeros(max_words, np.uint8)
+        ops = np.zeros((max_words, 3), np.uint64)
+        states = np.zeros(max_words, np.uint64)
+        st, nw = C.c_uint64(state), C.c_size_t()
+        _check(lib().bchk_sweep_range(self._h, snr_db, C.byref(st), draws, max_words, _p(tx), _p(res), _p(acc),
+                                      _p(ops), _p(states), C.byref(nw)))
+        B = nw.value
+        return tx[:B], res[:B], acc[:B], ops[:B], states[:B], st.value
+
     def sweep(self, p, e, max_snr=5.0, seed=1, batch=0, state=0, return_state=False):
         """fun() on the GPU: the reference CSV text (and the engine state after it)."""
         buf = C.create_string_buffer(1 << 16)
@@ -398,6 +416,24 @@ class PolarListDecoder:
 
     def sync(self):
         _check(lib().bchk_polar_sync(self._h))
+
+
+def stream_skip(k, n, state, words):
+    """(engine state, draws) after `words` stream words from `state` (no samples, no device)."""
+    st, dr = C.c_uint64(), C.c_uint64()
+    _check(lib().bchk_stream_skip(k, n, state, words, C.byref(st), C.byref(dr)))
+    return st.value, dr.value
+
+
+def stream_sync(k, n, state, offset, limit):
+    """The first word start at or after `offset` draws from word start `state`, without parsing
+    the draws before it: (draws from state, engine state), or None when unresolved."""
+    off, st = C.c_uint64(), C.c_uint64()
+    rc = lib().bchk_stream_sync(k, n, state, offset, limit, C.byref(off), C.byref(st))
+    if rc == 1:
+        return None
+    _check(rc)
+    return off.value, st.value
 
 
 def rng_jump(state, draws):

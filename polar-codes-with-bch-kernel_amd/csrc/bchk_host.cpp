@@ -26,6 +26,7 @@
 #include "bchk.h"
 #include "bchk_device.h"
 #include "bchk_launch.h"
+#include "bchk_stream.h"
 
 
 using namespace bchk;
@@ -1003,23 +1004,9 @@ int bchk_count_device(bchk_ctx *c, const uint8_t *d_tx, const uint8_t *d_res, co
 
 // The reference's stream: std::default_random_engine (seed 1 unless RANDOM is defined,
 // src/bchCoder.cpp:14-22), uniform_int_distribution<unsigned short>(0, 1) for the
-// information bits and a fresh normal_distribution(0, sd) per addNoise call.
+// information bits and a fresh normal_distribution(0, sd) per addNoise call -- drawn from
+// Minstd0 (bchk_stream.h), the same engine with its state readable.
 }  // extern "C"
-
-// The reference's engine with a count of its draws (the distributions see the same
-// result_type, min, max and values, so the stream is unchanged).
-struct CountingEngine {
-    using Eng = std::default_random_engine;
-    using result_type = Eng::result_type;
-    Eng &e;
-    uint64_t n = 0;
-    static constexpr result_type min() { return Eng::min(); }
-    static constexpr result_type max() { return Eng::max(); }
-    result_type operator()() {
-        ++n;
-        return e();
-    }
-};
 
 template <class Eng>
 static void gen_word(Eng &eng, const bchk_ctx *c, double sd, uint8_t *tx, double *y,
@@ -1032,6 +1019,61 @@ static void gen_word(Eng &eng, const bchk_ctx *c, double sd, uint8_t *tx, double
             for (size_t j = 0; j < c->g.size(); ++j) tx[i + j] ^= c->g[j];
     std::normal_distribution<double> noise(0.0, sd);
     for (int i = 0; i < c->n; ++i) y[i] = (tx[i] ? 1 : -1) + noise(eng);
+}
+
+// host threads for generating words: the job's CPU share (OMP_NUM_THREADS on the GPU box),
+// at most 16
+static int gen_threads() {
+    int t = (int)std::thread::hardware_concurrency();
+    if (const char *e = getenv("OMP_NUM_THREADS")) t = std::min(t > 0 ? t : 1, std::max(1, atoi(e)));
+    if (const char *e = getenv("BCHK_GEN_THREADS")) t = std::max(1, atoi(e));
+    return std::max(1, std::min(t, 16));
+}
+
+// `start` holds B + 1 word-start states (start[b] = engine state before word b, from the
+// sample-free parse); the B words are generated by up to gen_threads() threads, each from its
+// words' own start states, so the rows are the sequential stream's.
+static int gen_from_starts(const bchk_ctx *c, double sd, const std::vector<uint64_t> &start, size_t B, uint8_t *tx,
+                           double *y) {
+    const size_t n = (size_t)c->n;
+    const int T = (int)std::min<size_t>((size_t)gen_threads(), std::max<size_t>(1, B / 1024));
+    std::vector<int> bad(T, 0);
+    auto work = [&](int q) {
+        std::vector<uint8_t> info(c->k);
+        for (size_t b = B * q / T; b < B * (q + 1) / T; ++b) {
+            Minstd0 e(start[b]);
+            gen_word(e, c, sd, tx + b * n, y + b * n, info);
+            bad[q] |= e.x != start[b + 1];  // the parse and the distributions agree on every word
+        }
+    };
+    std::vector<std::thread> th;
+    for (int q = 1; q < T; ++q) th.emplace_back(work, q);
+    work(0);
+    for (auto &t : th) t.join();
+    for (int q = 0; q < T; ++q)
+        if (bad[q]) return fail(BCHK_EINVAL, "stream parse and generator disagree (internal error)");
+    return 0;
+}
+
+// B words from engine state *x (advanced past them); after[b] (may be NULL) = the state after
+// word b; *draws (may be NULL) = the engine draws the words consumed.
+static int gen_words(const bchk_ctx *c, double sd, uint64_t *x, size_t B, uint8_t *tx, double *y, uint64_t *after,
+                     uint64_t *draws) {
+    const int pairs = (c->n + 1) / 2;
+    std::vector<uint64_t> start(B + 1);
+    start[0] = Minstd0(*x).x;
+    uint64_t d = 0;
+    for (size_t b = 0; b < B; ++b) {
+        uint64_t xx = start[b];
+        d += stream_skip_word(xx, c->k, pairs);
+        start[b + 1] = xx;
+    }
+    if (int rc = gen_from_starts(c, sd, start, B, tx, y)) return rc;
+    if (after)
+        for (size_t b = 0; b < B; ++b) after[b] = start[b + 1];
+    *x = start[B];
+    if (draws) *draws = d;
+    return 0;
 }
 
 extern "C" {
@@ -1061,44 +1103,18 @@ uint64_t bchk_rng_jump(uint64_t state, uint64_t draws) {
 int bchk_generate_host_draws(const bchk_ctx *c, double snr_db, size_t B, uint64_t *rng_state, uint64_t seed,
                              uint8_t *tx, double *y, uint64_t *draws) {
     if (!c || (B && (!tx || !y))) return fail(BCHK_EINVAL, "NULL argument");
-    std::default_random_engine eng(minstd_state(rng_state && *rng_state ? *rng_state : seed));
-    CountingEngine ce{eng};
-    std::vector<uint8_t> info(c->k);
-    const double sd = sweep_sigma(c, snr_db);
-    for (size_t b = 0; b < B; ++b) gen_word(ce, c, sd, tx + b * c->n, y + b * c->n, info);
-    if (rng_state) {
-        std::stringstream ss;
-        ss << eng;
-        ss >> *rng_state;
-    }
-    if (draws) *draws = ce.n;
+    uint64_t x = minstd_state(rng_state && *rng_state ? *rng_state : seed);
+    if (int rc = gen_words(c, sweep_sigma(c, snr_db), &x, B, tx, y, nullptr, draws)) return rc;
+    if (rng_state) *rng_state = x;
     return 0;
 }
 
-int bchk_sweep_block(bchk_ctx *c, double snr_db, uint64_t *rng_state, size_t skip, size_t B, uint8_t *tx,
-                     uint8_t *res, uint8_t *accepted, uint64_t *ops, uint64_t *states) {
-    if (!c || !rng_state || (B && (!tx || !res || !accepted || !ops || !states)))
-        return fail(BCHK_EINVAL, "NULL argument");
-    std::default_random_engine eng(minstd_state(*rng_state));
-    std::vector<uint8_t> info(c->k), junk(c->n);
-    std::vector<double> yj(c->n), y(B * c->n);
-    const double sd = sweep_sigma(c, snr_db);
-    for (size_t b = 0; b < skip; ++b) gen_word(eng, c, sd, junk.data(), yj.data(), info);
-    for (size_t b = 0; b < B; ++b) {
-        gen_word(eng, c, sd, tx + b * c->n, y.data() + b * c->n, info);
-        std::stringstream ss;
-        ss << eng;
-        ss >> states[b];
-    }
-    {
-        std::stringstream ss;
-        ss << eng;
-        ss >> *rng_state;
-    }
+// decode B generated words on the GPU: res rows zeroed, then written on acceptance
+static int sweep_decode(bchk_ctx *c, const double *y, size_t B, uint8_t *res, uint8_t *accepted, uint64_t *ops) {
     if (B == 0) return 0;
     std::vector<bchk_stats> st(B);
     memset(res, 0, B * c->n);
-    if (int rc = bchk_decode_host(c, y.data(), B, res, nullptr, st.data())) return rc;
+    if (int rc = bchk_decode_host(c, y, B, res, nullptr, st.data())) return rc;
     for (size_t b = 0; b < B; ++b) {
         accepted[b] = (st[b].flags & BCHK_F_ACCEPTED) ? 1 : 0;
         ops[3 * b] = st[b].decodes;
@@ -1108,24 +1124,46 @@ int bchk_sweep_block(bchk_ctx *c, double snr_db, uint64_t *rng_state, size_t ski
     return 0;
 }
 
+int bchk_sweep_block(bchk_ctx *c, double snr_db, uint64_t *rng_state, size_t skip, size_t B, uint8_t *tx,
+                     uint8_t *res, uint8_t *accepted, uint64_t *ops, uint64_t *states) {
+    if (!c || !rng_state || (B && (!tx || !res || !accepted || !ops || !states)))
+        return fail(BCHK_EINVAL, "NULL argument");
+    uint64_t x = minstd_state(*rng_state);
+    const int pairs = (c->n + 1) / 2;
+    for (size_t b = 0; b < skip; ++b) stream_skip_word(x, c->k, pairs);  // other ranks' words: draws only
+    std::vector<double> y(B * c->n);
+    if (int rc = gen_words(c, sweep_sigma(c, snr_db), &x, B, tx, y.data(), states, nullptr)) return rc;
+    *rng_state = x;
+    return sweep_decode(c, y.data(), B, res, accepted, ops);
+}
+
+int bchk_sweep_range(bchk_ctx *c, double snr_db, uint64_t *rng_state, uint64_t draws, size_t max_words,
+                     uint8_t *tx, uint8_t *res, uint8_t *accepted, uint64_t *ops, uint64_t *states, size_t *words) {
+    if (!c || !rng_state || !words || (max_words && (!tx || !res || !accepted || !ops || !states)))
+        return fail(BCHK_EINVAL, "NULL argument");
+    const int pairs = (c->n + 1) / 2;
+    std::vector<uint64_t> start(1, minstd_state(*rng_state));
+    uint64_t d = 0;
+    while (d < draws) {  // the words of the range, found by the sample-free parse
+        if (start.size() > max_words) return fail(BCHK_EINVAL, "range holds more than %zu words", max_words);
+        uint64_t xx = start.back();
+        d += stream_skip_word(xx, c->k, pairs);
+        start.push_back(xx);
+    }
+    if (d != draws) return fail(BCHK_EINVAL, "the range does not end on a word boundary (%llu != %llu draws)",
+                                (unsigned long long)d, (unsigned long long)draws);
+    const size_t B = start.size() - 1;
+    std::vector<double> y(B * c->n);
+    if (int rc = gen_from_starts(c, sweep_sigma(c, snr_db), start, B, tx, y.data())) return rc;
+    for (size_t b = 0; b < B; ++b) states[b] = start[b + 1];
+    *rng_state = start[B];
+    *words = B;
+    return sweep_decode(c, y.data(), B, res, accepted, ops);
+}
+
 int bchk_generate_host(const bchk_ctx *c, double snr_db, size_t B, uint64_t *rng_state, uint64_t seed,
                        uint8_t *tx, double *y) {
-    if (!c || (B && (!tx || !y))) return fail(BCHK_EINVAL, "NULL argument");
-    std::default_random_engine eng(rng_state && *rng_state ? *rng_state : seed);
-    if (rng_state && *rng_state) {
-        std::stringstream ss;
-        ss << *rng_state;
-        ss >> eng;
-    }
-    std::vector<uint8_t> info(c->k);
-    const double sd = sweep_sigma(c, snr_db);
-    for (size_t b = 0; b < B; ++b) gen_word(eng, c, sd, tx + b * c->n, y + b * c->n, info);
-    if (rng_state) {
-        std::stringstream ss;
-        ss << eng;
-        ss >> *rng_state;
-    }
-    return 0;
+    return bchk_generate_host_draws(c, snr_db, B, rng_state, seed, tx, y, nullptr);
 }
 
 // On-GPU channel (bchk_channel.hip): words [word0, word0 + B) of the counter-based stream
@@ -1249,16 +1287,11 @@ int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t *rng_state,
     if (p <= 0 || e <= 0) return fail(BCHK_EINVAL, "p and e must be positive");
     const size_t n = c->n;
     const size_t max_batch = batch ? batch : (size_t(1) << 18);
-    std::default_random_engine eng(seed);
-    if (rng_state && *rng_state) {
-        std::stringstream ss;
-        ss << *rng_state;
-        ss >> eng;
-    }
-    std::vector<uint8_t> info(c->k), tx, res, dec(n, 0);
+    uint64_t x = minstd_state(rng_state && *rng_state ? *rng_state : seed);
+    std::vector<uint8_t> tx, res, dec(n, 0);
     std::vector<double> y;
     std::vector<bchk_stats> st;
-    std::vector<std::default_random_engine> snap;
+    std::vector<uint64_t> after;  // engine state after each word of the batch
     std::ostringstream out;
     int count = 0, countErr = 0, countE = 0;  // int, as src/dataForPlot.cpp:20
     unsigned long D = 0, Cc = 0, Ss = 0, wordCount = 0;
@@ -1275,12 +1308,9 @@ int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t *rng_state,
             y.resize(nb * n);
             res.assign(nb * n, 0);
             st.resize(nb);
-            snap.resize(nb + 1);
-            for (size_t b = 0; b < nb; ++b) {
-                snap[b] = eng;
-                gen_word(eng, c, sd, &tx[b * n], &y[b * n], info);
-            }
-            snap[nb] = eng;
+            after.resize(nb);
+            const uint64_t x0 = x;
+            if (int rc = gen_words(c, sd, &x, nb, tx.data(), y.data(), after.data(), nullptr)) return rc;
             int rc = bchk_decode_host(c, y.data(), nb, res.data(), nullptr, st.data());
             if (rc) return rc;
             size_t used = 0;
@@ -1299,7 +1329,7 @@ int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t *rng_state,
                 Ss += st[b].sums;
                 used = b + 1;
             }
-            eng = snap[used];  // rewind the stream to the first word not consumed
+            x = used ? after[used - 1] : x0;  // rewind the stream to the first word not consumed
             fer_est = std::max(1e-7, (double)(errs_batch + 1) / (double)(used + 1));
         }
         out << stnr << "," << ((double)countErr) / count << "," << ((double)countE) / count / (long)n << ","
@@ -1309,11 +1339,7 @@ int bchk_sweep(bchk_ctx *c, long p, long e, double max_snr, uint64_t *rng_state,
         wordCount = 0;
         count = 0, countErr = 0;
     }
-    if (rng_state) {
-        std::stringstream ss;
-        ss << eng;
-        ss >> *rng_state;
-    }
+    if (rng_state) *rng_state = x;
     const std::string s = out.str();
     if (s.size() + 1 > cap) return fail(BCHK_EINVAL, "csv buffer too small (%zu needed)", s.size() + 1);
     memcpy(csv, s.c_str(), s.size() + 1);

@@ -215,7 +215,7 @@ int run_costs(const uint8_t *K, int l, int m, const float *llr, uint64_t ncodes,
 extern "C" {
 
 int bchk_kernel_ebch(int power, uint8_t *K) {
-    if (power < 2 || power > 5 || !K) return kfail(BCHK_EINVAL, "power %d unsupported (2..5)", power);
+    if (power < 2 || power > 6 || !K) return kfail(BCHK_EINVAL, "power %d unsupported (2..6)", power);
     const int len = (1 << power) - 1, N = len + 1, n = len;
     const int amount = (power != 2) ? ((1 << power) - 2) / 2 : 2;
     std::vector<unsigned> alog(n);
@@ -267,7 +267,7 @@ int bchk_kernel_ebch(int power, uint8_t *K) {
 }
 
 int bchk_kernel_field_order(int power, const uint8_t *K, uint8_t *out) {
-    if (power < 2 || power > 5 || !K || !out) return kfail(BCHK_EINVAL, "power %d unsupported (2..5)", power);
+    if (power < 2 || power > 6 || !K || !out) return kfail(BCHK_EINVAL, "power %d unsupported (2..6)", power);
     const int n = 1 << power;
     std::vector<unsigned> alog(n - 1);
     for (unsigned i = 0, v = 1; i < (unsigned)(n - 1); ++i) {

@@ -35,11 +35,19 @@ constexpr int polar_path_c(int U) { return ((3 * U + 15) & ~15) + 16; }
 constexpr int polar_rec_words(int K) { return K > 0 ? (K + 31) / 32 : 1; }
 
 // Mixed kernels (polar_mixed.hip): layer j has a kernel of size ksize[j] (Arikan or a
-// matrix, rows as bitmasks krows[j * kPolarMaxKernel + r], bit c = K[r][c]); outer[λ] =
+// matrix, rows as 64-bit masks krows[j * kPolarMaxKernel + r], bit c = K[r][c]); outer[λ] =
 // U / (ksize[0] ... ksize[λ-1]); per path S layer λ at soff[λ] (outer[λ] floats, λ >= 1), C
 // layer λ at coff[λ] (outer[λ] ksize[λ-1] bytes, C_0 = U), matrix offset states at ooff[j].
-constexpr int kPolarMaxKernel = 32;
-constexpr int kPolarMaxMatrixGpu = 32;  // as CTrellisKernelProcessor (< 64), rows as u32 masks
+constexpr int kPolarMaxKernel = 64;
+constexpr int kPolarMaxMatrixGpu = 64;  // the 2^6 extended-BCH kernel (CTrellisKernelProcessor: < 64)
+constexpr int kPolarMaxTrellisKernel = 32;  // the trellis is built for kernels up to 32 only
+// Matrix layers of size > 32 (or from BCHK_POLAR_ML up) take their LLRs from an exact
+// ordered-statistics search instead (one wave per item, polar_mixed.hip ml_llr): per wave an
+// LDS scratch of kMlStack 16-byte search nodes, the reduced basis (64 u64), flip costs and
+// |y| (64 floats each). Phases whose coset has at most 2^kMlEnumBits words are enumerated.
+constexpr int kMlStack = 2048;
+constexpr int kMlEnumBits = 10;
+constexpr uint32_t kMlScratchBytes = 16u * kMlStack + 8u * 64u + 4u * 64u + 4u * 64u;
 // Matrix layers of size >= the trellis threshold (default 16, BCHK_POLAR_TRELLIS) take their
 // LLRs from CTrellisKernelProcessor's trellis (pull-form Viterbi over predecessor lists);
 // smaller ones enumerate the coset (2^(size - 1 - phase) words per LLR). Per (layer, phase):
@@ -58,7 +66,7 @@ struct PolarMixedParams {
     const uint16_t *phase;
     const uint64_t *dfcorr;
     const int16_t *cwpos;
-    const uint32_t *krows;  // [nl][kPolarMaxKernel]
+    const uint64_t *krows;  // [nl][kPolarMaxKernel]
     const uint32_t *tent, *tbase;  // trellis predecessor lists (see above)
     const uint8_t *tlog;
     int32_t tstates;               // largest state count of any trellis layer (>= 64 if any)
@@ -69,18 +77,22 @@ struct PolarMixedParams {
     int32_t soff[kPolarMaxLayers + 1], coff[kPolarMaxLayers + 1], ooff[kPolarMaxLayers];
     uint8_t arikan[kPolarMaxLayers];
     uint8_t trellis[kPolarMaxLayers];  // matrix layer decoded through its trellis
+    uint8_t ml[kPolarMaxLayers];       // matrix layer decoded by the ordered-statistics search
+    int32_t any_ml;                    // LDS holds the search scratch
 };
 
 inline uint32_t polar_mixed_lds_bytes(int U, int L, int K, int ssize, int csize, int osize, int nl,
-                                      int tstates) {
+                                      int tstates, bool ml) {
     uint32_t b = (4u * (uint32_t)U + 15u) & ~15u;                                     // channel
     b += 4u * (uint32_t)ssize * (uint32_t)L + (uint32_t)csize * (uint32_t)L;           // S, C
     b = (b + (uint32_t)osize * (uint32_t)L + 15u) & ~15u;                              // offsets
     b = (b + 2u * (uint32_t)U + 15u) & ~15u;                                           // phases
-    b += 4u * (uint32_t)kPolarMaxKernel * (uint32_t)nl;                                // rows
+    b += 8u * (uint32_t)kPolarMaxKernel * (uint32_t)nl;                                // rows
     b += 4u * (uint32_t)L + 4u * (uint32_t)L * (uint32_t)polar_rec_words(K);            // act, rec
     b = (b + 15u) & ~15u;
     b += 8u * (uint32_t)tstates;  // trellis state metrics: two buffers of tstates floats
+    b = (b + 15u) & ~15u;
+    if (ml) b += kMlScratchBytes;  // ordered-statistics search scratch
     return (b + 15u) & ~15u;
 }
 

@@ -77,7 +77,7 @@ struct bchk_polar {
     bool mixed = false;
     std::vector<int> ksize;
     std::vector<uint8_t> arikan;
-    std::vector<uint32_t> krows;  // [layer][kPolarMaxKernel]
+    std::vector<uint64_t> krows;  // [layer][kPolarMaxKernel]
     PolarMixedParams mp{};        // the mixed layout (sizes, offsets)
     size_t off_krows = 0;
     std::vector<uint32_t> tent, tbase;  // matrix-layer trellises (polar_device.h)
@@ -105,7 +105,7 @@ namespace {
 // GetKernelByName (Kernel.cpp:235-252): "A" (any case), or a matrix file "-path" / "<path"
 // (relative to kdir) holding the size and size^2 entries (Kernel.cpp:93-107); the kernel must
 // be invertible (Kernel.cpp:155-176).
-int read_kernel(const std::string &name, const char *kdir, int *size, uint32_t *rows, bool *arikan) {
+int read_kernel(const std::string &name, const char *kdir, int *size, uint64_t *rows, bool *arikan) {
     if (name == "A" || name == "a") {
         *size = 2;
         rows[0] = 1u;       // 1 0
@@ -131,18 +131,18 @@ int read_kernel(const std::string &name, const char *kdir, int *size, uint32_t *
                 fclose(f);
                 return pfail(BCHK_EINVAL, "Error parsing kernel file %s", path.c_str());
             }
-            if (v) rows[r] |= 1u << q;
+            if (v) rows[r] |= 1ull << q;
         }
     }
     fclose(f);
-    std::vector<uint32_t> a(rows, rows + l);  // GF(2) rank
+    std::vector<uint64_t> a(rows, rows + l);  // GF(2) rank
     for (int col = 0, r0 = 0; col < l; ++col) {
         int piv = r0;
-        while (piv < l && !((a[piv] >> col) & 1u)) ++piv;
+        while (piv < l && !((a[piv] >> col) & 1ull)) ++piv;
         if (piv == l) return pfail(BCHK_EINVAL, "Kernel is singular (%s)", path.c_str());
         std::swap(a[piv], a[r0]);
         for (int r = 0; r < l; ++r)
-            if (r != r0 && ((a[r] >> col) & 1u)) a[r] ^= a[r0];
+            if (r != r0 && ((a[r] >> col) & 1ull)) a[r] ^= a[r0];
         ++r0;
     }
     if (l > kPolarMaxMatrixGpu)
@@ -159,7 +159,8 @@ int read_kernel(const std::string &name, const char *kdir, int *size, uint32_t *
 // stored as predecessor lists for the GPU's pull-form Viterbi (polar_device.h). Appends to
 // ent; base[phase], lg[phase * (kPolarMaxKernel + 1) + d]; returns the largest state count
 // (0 and a message when a depth needs more than 2^kPolarTrellisMaxBits states).
-int build_trellis(const uint32_t *rows, int l, std::vector<uint32_t> &ent, uint32_t *base, uint8_t *lg) {
+int build_trellis(const uint64_t *rows, int l, std::vector<uint32_t> &ent, uint32_t *base, uint8_t *lg) {
+    if (l > kPolarMaxTrellisKernel) return pfail(BCHK_EINVAL, "no trellis for a kernel of size %d (> %d)", l, kPolarMaxTrellisKernel), 0;
     int most = 1;
     const unsigned N = (unsigned)l + 1u;
     for (int ph = 0; ph < l; ++ph) {
@@ -268,7 +269,7 @@ int parse_spec(bchk_polar *c, const char *spec, const char *kdir) {
     if (layers < 1 || layers > kPolarMaxLayers) return pfail(BCHK_EINVAL, "%d layers unsupported", layers);
     c->ksize.assign(layers, 2);
     c->arikan.assign(layers, 1);
-    c->krows.assign((size_t)layers * kPolarMaxKernel, 0u);
+    c->krows.assign((size_t)layers * kPolarMaxKernel, 0ull);
     long Ul = 1;
     for (int i = 0; i < layers; ++i) {
         std::string name;
@@ -379,15 +380,21 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
         m.ssize = (so + 3) & ~3;
         m.csize = (co + 15) & ~15;
         m.osize = (oo + 15) & ~15;
-        // matrix layers from the trellis threshold up take their LLRs from the trellis
-        int tmin = 16;
+        // matrix layers from the trellis threshold up take their LLRs from the trellis; those
+        // larger than the trellis limit (or from BCHK_POLAR_ML up) from the exact
+        // ordered-statistics search
+        int tmin = 16, mlmin = kPolarMaxTrellisKernel + 1;
         if (const char *e = getenv("BCHK_POLAR_TRELLIS")) tmin = std::max(2, atoi(e));
+        if (const char *e = getenv("BCHK_POLAR_ML")) mlmin = std::max(2, atoi(e));
+        m.any_ml = 0;
         m.tstates = 0;
         c->tbase.assign((size_t)nl * kPolarMaxKernel, 0u);
         c->tlog.assign((size_t)nl * kPolarMaxKernel * (kPolarMaxKernel + 1), 0u);
         c->tent.clear();
         for (int j = 0; j < nl; ++j) {
-            m.trellis[j] = (!c->arikan[j] && c->ksize[j] >= tmin) ? 1 : 0;
+            m.ml[j] = (!c->arikan[j] && c->ksize[j] >= std::min(mlmin, kPolarMaxTrellisKernel + 1)) ? 1 : 0;
+            m.any_ml |= m.ml[j];
+            m.trellis[j] = (!c->arikan[j] && !m.ml[j] && c->ksize[j] >= tmin) ? 1 : 0;
             if (!m.trellis[j]) continue;
             const int most = build_trellis(&c->krows[(size_t)j * kPolarMaxKernel], c->ksize[j], c->tent,
                                            &c->tbase[(size_t)j * kPolarMaxKernel],
@@ -399,7 +406,7 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
             m.tstates = std::max(m.tstates, std::max(64, most));
         }
         if (c->tent.empty()) c->tent.push_back(0u);
-        c->lds = polar_mixed_lds_bytes(c->U, c->L, c->K, m.ssize, m.csize, m.osize, nl, m.tstates);
+        c->lds = polar_mixed_lds_bytes(c->U, c->L, c->K, m.ssize, m.csize, m.osize, nl, m.tstates, m.any_ml != 0);
     } else {
         c->lds = polar_lds_bytes(c->U, c->L, c->K);
     }
@@ -434,7 +441,7 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
     c->off_phase = o; o = al(o + 2 * (size_t)c->U);
     c->off_cwpos = o; o = al(o + 2 * (size_t)c->N);
     c->off_dfcorr = o; o = al(o + 8 * (size_t)c->U);
-    c->off_krows = o; o = al(o + 4 * c->krows.size());
+    c->off_krows = o; o = al(o + 8 * c->krows.size());
     c->off_tent = o; o = al(o + 4 * c->tent.size());
     c->off_tbase = o; o = al(o + 4 * c->tbase.size());
     c->off_tlog = o; o = al(o + c->tlog.size());
@@ -448,7 +455,7 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
     }
     memcpy(blob.data() + c->off_cwpos, c->cwpos.data(), 2 * (size_t)c->N);
     memcpy(blob.data() + c->off_dfcorr, c->dfcorr.data(), 8 * (size_t)c->U);
-    memcpy(blob.data() + c->off_krows, c->krows.data(), 4 * c->krows.size());
+    memcpy(blob.data() + c->off_krows, c->krows.data(), 8 * c->krows.size());
     if (!c->tent.empty()) memcpy(blob.data() + c->off_tent, c->tent.data(), 4 * c->tent.size());
     if (!c->tbase.empty()) memcpy(blob.data() + c->off_tbase, c->tbase.data(), 4 * c->tbase.size());
     if (!c->tlog.empty()) memcpy(blob.data() + c->off_tlog, c->tlog.data(), c->tlog.size());
@@ -529,7 +536,7 @@ int bchk_polar_decode_device(bchk_polar *c, const float *d_llr, size_t B, uint8_
         m.phase = p.phase;
         m.dfcorr = p.dfcorr;
         m.cwpos = p.cwpos;
-        m.krows = reinterpret_cast<const uint32_t *>(c->d_tab + c->off_krows);
+        m.krows = reinterpret_cast<const uint64_t *>(c->d_tab + c->off_krows);
         m.tent = reinterpret_cast<const uint32_t *>(c->d_tab + c->off_tent);
         m.tbase = reinterpret_cast<const uint32_t *>(c->d_tab + c->off_tbase);
         m.tlog = c->d_tab + c->off_tlog;
@@ -598,12 +605,12 @@ int bchk_polar_encode_host(const bchk_polar *c, const uint8_t *info, size_t B, u
         std::vector<uint8_t> t(c->U);
         for (int L = c->n - 1, stride = 1; L >= 0; --L) {
             const int l = c->ksize[L], next = stride * l;
-            const uint32_t *kr = &c->krows[(size_t)L * kPolarMaxKernel];
+            const uint64_t *kr = &c->krows[(size_t)L * kPolarMaxKernel];
             for (int b0 = 0; b0 < c->U; b0 += next)
                 for (int i = 0; i < l; ++i)
                     for (int s2 = 0; s2 < stride; ++s2) {
                         uint8_t acc = 0;
-                        for (int j = 0; j < l; ++j) acc ^= (uint8_t)(u[b0 + j * stride + s2] & ((kr[j] >> i) & 1u));
+                        for (int j = 0; j < l; ++j) acc ^= (uint8_t)(u[b0 + j * stride + s2] & ((kr[j] >> i) & 1ull));
                         t[b0 + i * stride + s2] = acc;
                     }
             u.swap(t);

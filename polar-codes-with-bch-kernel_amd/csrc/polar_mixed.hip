@@ -69,24 +69,194 @@ struct MStack {  // TVMemoryEngine's path-index stack with lazy initialisation (
 
 // min over the words of one half of the coset (CTrellisKernelProcessor::GetLLRs, :272-292):
 // words c = XOR of rows phase+1 .. l-1 selected by v, v = first, first + step, ...; metric of
-// c (b = 0) and c ^ row[phase] (b = 1) against the hard decision
-__device__ __forceinline__ void coset_min(const uint32_t *rows, int l, int phase, const float *ay, uint32_t hd,
+// c (b = 0) and c ^ row[phase] (b = 1) against the hard decision (l <= 32)
+__device__ __forceinline__ void coset_min(const uint64_t *rows, int l, int phase, const float *ay, uint64_t hd,
                                           uint32_t first, uint32_t step, float &b0, float &b1) {
     const int nfree = l - phase - 1;
     const uint32_t nw = 1u << nfree;
     for (uint32_t v = first; v < nw; v += step) {
-        uint32_t c = 0;
+        uint64_t c = 0;
         for (int r = 0; r < nfree; ++r)
             if ((v >> r) & 1u) c ^= rows[phase + 1 + r];
-        const uint32_t d0 = c ^ hd, d1 = d0 ^ rows[phase];
+        const uint64_t d0 = c ^ hd, d1 = d0 ^ rows[phase];
         float m0 = 0.0f, m1 = 0.0f;  // left to right (:279-282)
         for (int j = 0; j < l; ++j) {
-            if ((d0 >> j) & 1u) m0 += ay[j];
-            if ((d1 >> j) & 1u) m1 += ay[j];
+            if ((d0 >> j) & 1ull) m0 += ay[j];
+            if ((d1 >> j) & 1ull) m1 += ay[j];
         }
         b0 = m0 < b0 ? m0 : b0;
         b1 = m1 < b1 ? m1 : b1;
     }
+}
+
+
+// ---- exact kernel LLRs by an ordered-statistics search (matrix kernels beyond the trellis
+// limit, e.g. the 64 x 64 extended-BCH kernel of root bchCoder.cpp:356-389 makeMatrix).
+// The value is CTrellisKernelProcessor's (:234-294): best[1] - best[0], best[b] the least
+// left-to-right float sum of |y| over the disagreeing positions of a word of rows phase+1..l-1
+// (b = 0) or of those words plus row `phase` (b = 1). Gauss-Jordan over the positions in
+// decreasing |y| gives the most reliable basis of rows phase+1..l-1 (the pivots); a word of
+// half b is fixed by its pivot values, and the one matching the hard decision there is the
+// root. Flipping a set E of pivots costs at least the sum of their |y| (those positions then
+// disagree), so a search over E, cheapest pivot first, that drops every subtree whose flip cost
+// exceeds the best metric found (less a float-rounding margin) still visits every word that
+// can be a minimum: the result is the coset enumeration's, bit for bit. The wave works on one
+// item: 64 lanes sort the positions and eliminate (a lane per row), then evaluate 64 search
+// nodes per round (a node per lane) from a LIFO in LDS.
+struct MlNode {  // the words c ^ Gs[i] (and below them): flip cost so far lb, half b
+    uint64_t c;
+    float lb;
+    uint16_t i, b;
+};
+struct MlScratch {
+    uint64_t *G;   // [64] reduced basis, by increasing flip cost
+    float *cost;   // [64] flip cost of each basis row (|y| at its pivot)
+    float *ay;     // [64] |y| by position
+    MlNode *stk;   // [kMlStack]
+};
+// a subtree is dropped when lb * kMlShrink > best: a float sum of at most 64 non-negative terms
+// is within 64 u (u = 2^-24) of the exact sum, for lb and for every metric, so the margin
+// 2^-15 > 2 * 64 u keeps every word whose float metric could be <= best
+constexpr float kMlShrink = 1.0f - 1.0f / 32768.0f;
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ float wave_minf(float v) {
+    for (int m = 1; m < 64; m <<= 1) {
+        const float o = __shfl_xor(v, m, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_xor64(uint64_t v) {
+    for (int m = 1; m < 64; m <<= 1) v ^= shfl_xor64(v, m);
+    return v;
+}
+// the metric of the word whose disagreement mask is dis: |y| summed in index order (adding
+// +0 where a position agrees leaves the sum unchanged, so this is the trellis's path sum)
+__device__ __forceinline__ float ml_metric(uint64_t dis, const float *ay, int l) {
+    float m = 0.0f;
+    for (int j = 0; j < l; ++j) m += ((dis >> j) & 1ull) ? ay[j] : 0.0f;
+    return m;
+}
+
+__device__ float ml_llr(const uint64_t *kr, int l, int loc, const float *src, const uint8_t *off, int d, int s,
+                        int lane, const MlScratch &ms) {
+    // the layer's LLRs with the known inputs' sign flips (:240-262), HD = Y < 0 (:270-276)
+    float a = 0.0f;
+    bool neg = false;
+    if (lane < l) {
+        const float v = src[lane * d + s];
+        const float yv = off[lane * d + s] ? -v : v;
+        neg = yv < 0.0f;
+        a = fabsf(yv);
+        ms.ay[lane] = a;
+    }
+    const uint64_t hd = __ballot(neg);
+    wsync();
+    const int nf = l - loc - 1;
+    const float kInf = __int_as_float(0x7F800000);
+    if (nf <= kMlEnumBits) {  // small coset: enumerated, words spread over the lanes
+        float b0 = kInf, b1 = kInf;
+        for (uint32_t v = (uint32_t)lane; v < (1u << nf); v += 64) {
+            uint64_t c = 0;
+            for (int r = 0; r < nf; ++r)
+                if ((v >> r) & 1u) c ^= kr[loc + 1 + r];
+            const float m0 = ml_metric(c ^ hd, ms.ay, l), m1 = ml_metric(c ^ hd ^ kr[loc], ms.ay, l);
+            b0 = m0 < b0 ? m0 : b0;
+            b1 = m1 < b1 ? m1 : b1;
+        }
+        return wave_minf(b1) - wave_minf(b0);
+    }
+    // positions by decreasing |y| (bitonic across the lanes; key: |y| bits, valid, position)
+    uint64_t key = lane < l ? (((uint64_t)__float_as_uint(a) << 8) | 0x80ull | (uint64_t)(63 - lane)) : 0ull;
+    for (int k = 2; k <= 64; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t o = shfl_xor64(key, j);
+            const bool desc = (lane & k) == 0, lower = (lane & j) == 0;
+            key = (lower == desc) ? (o > key ? o : key) : (o < key ? o : key);
+        }
+    const int pos = 63 - (int)(key & 63ull);
+    // Gauss-Jordan: lane i < nf holds row loc + 1 + i; pivots in decreasing |y|
+    uint64_t g = lane < nf ? kr[loc + 1 + lane] : 0ull;
+    bool used = false;
+    int t = 0, piv = 0;
+    for (int si = 0, np = 0; si < l && np < nf; ++si) {
+        const int p = __builtin_amdgcn_readlane(pos, si);
+        const uint64_t cand = __ballot(lane < nf && !used && ((g >> p) & 1ull));
+        if (!cand) continue;
+        const int r = (int)__builtin_ctzll(cand);
+        const uint64_t gr = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), r) << 32);
+        if (lane == r) {
+            used = true;
+            t = np;
+            piv = p;
+        } else if (lane < nf && ((g >> p) & 1ull)) {
+            g ^= gr;
+        }
+        ++np;
+    }
+    if (lane < nf) {  // found in decreasing |y|: index nf - 1 - t runs by increasing cost
+        ms.G[nf - 1 - t] = g;
+        ms.cost[nf - 1 - t] = ms.ay[piv];
+    }
+    // the roots: the word of each half that matches the hard decision on the pivots
+    const uint64_t root0 = wave_xor64(lane < nf && ((hd >> piv) & 1ull) ? g : 0ull);
+    const uint64_t t1 = hd ^ kr[loc];
+    const uint64_t root1 = kr[loc] ^ wave_xor64(lane < nf && ((t1 >> piv) & 1ull) ? g : 0ull);
+    float best0 = ml_metric(root0 ^ hd, ms.ay, l), best1 = ml_metric(root1 ^ hd, ms.ay, l);
+    int sp = 0;
+    if (lane == 0) {
+        ms.stk[0] = MlNode{root0, 0.0f, 0, 0};
+        ms.stk[1] = MlNode{root1, 0.0f, 0, 1};
+    }
+    sp = 2;
+    wsync();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    // a guard only (the search tree is finite): past 2^20 rounds the LLR is NaN, never a hang
+    for (uint32_t rounds = 0; sp > 0; ++rounds) {
+        if (rounds >= (1u << 20)) return __int_as_float(0x7FC00000);
+        // the top n nodes, one per lane; n shrinks near the stack's end so that the pushes of a
+        // round (at most 2 per node) and of one depth-first descent (< 64) always fit
+        int n = sp < 64 ? sp : 64;
+        const int room = kMlStack - 128 - sp;
+        if (room < n) n = room > 1 ? room : 1;
+        const bool have = lane < n;
+        MlNode e{0ull, 0.0f, 0, 0};
+        if (have) e = ms.stk[sp - n + lane];
+        sp -= n;
+        wsync();
+        const int i = e.i;
+        const bool hb = e.b != 0;
+        const float bound = hb ? best1 : best0;
+        const float l2 = have ? e.lb + ms.cost[i] : kInf;
+        const bool live = have && l2 * kMlShrink <= bound;
+        uint64_t c2 = 0ull;
+        float m = kInf;
+        if (live) {
+            c2 = e.c ^ ms.G[i];
+            m = ml_metric(c2 ^ hd, ms.ay, l);
+        }
+        const float n0 = wave_minf(live && !hb ? m : kInf), n1 = wave_minf(live && hb ? m : kInf);
+        best0 = n0 < best0 ? n0 : best0;
+        best1 = n1 < best1 ? n1 : best1;
+        const float nb = hb ? best1 : best0;
+        const bool more = live && i + 1 < nf;
+        const float nc = more ? ms.cost[i + 1] : 0.0f;
+        const bool psib = more && (e.lb + nc) * kMlShrink <= nb;  // the next pivot instead of this one
+        const bool pch = more && (l2 + nc) * kMlShrink <= nb;     // this one and a later one
+        const uint64_t ms_ = __ballot(psib), mc = __ballot(pch);
+        const int nsib = __builtin_popcountll(ms_);
+        if (psib) ms.stk[sp + __builtin_popcountll(ms_ & lt)] = MlNode{e.c, e.lb, (uint16_t)(i + 1), e.b};
+        if (pch) ms.stk[sp + nsib + __builtin_popcountll(mc & lt)] = MlNode{c2, l2, (uint16_t)(i + 1), e.b};
+        sp += nsib + __builtin_popcountll(mc);
+        wsync();
+    }
+    return best1 - best0;  // (:292)
 }
 
 }  // namespace
@@ -102,17 +272,20 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
     const int o_O = o_C + p.csize * L;
     const int o_ph = (o_O + p.osize * L + 15) & ~15;
     const int o_rows = (o_ph + 2 * U + 15) & ~15;
-    const int o_act = o_rows + 4 * kPolarMaxKernel * nl;
+    const int o_act = o_rows + 8 * kPolarMaxKernel * nl;
     const int o_tm = (o_act + 4 * L + 4 * L * RW + 15) & ~15;
     float *chan = reinterpret_cast<float *>(smem);
     float *S = reinterpret_cast<float *>(smem + o_S);
     uint8_t *C = smem + o_C;
     uint8_t *O = smem + o_O;
     uint16_t *ph = reinterpret_cast<uint16_t *>(smem + o_ph);
-    uint32_t *rows = reinterpret_cast<uint32_t *>(smem + o_rows);  // [layer][row] bitmasks
+    uint64_t *rows = reinterpret_cast<uint64_t *>(smem + o_rows);  // [layer][row] bitmasks
     uint32_t *act = reinterpret_cast<uint32_t *>(smem + o_act);
     uint32_t *rec = act + L;
     float *tmet = reinterpret_cast<float *>(smem + o_tm);  // trellis state metrics, 2 x tstates
+    uint8_t *mls = smem + ((o_tm + 8 * p.tstates + 15) & ~15);  // ordered-statistics search scratch
+    MlScratch ms{reinterpret_cast<uint64_t *>(mls), reinterpret_cast<float *>(mls + 512),
+                 reinterpret_cast<float *>(mls + 768), reinterpret_cast<MlNode *>(mls + 1024)};
     const bool mine = lane < L;
     for (int i = lane; i < U; i += 64) ph[i] = p.phase[i];
     for (int i = lane; i < kPolarMaxKernel * nl; i += 64) rows[i] = p.krows[i];
@@ -177,7 +350,7 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                     continue;
                 }
                 // matrix layer: offset state (:240-262), then the min-sum LLR per element
-                const uint32_t *kr = rows + kPolarMaxKernel * j;
+                const uint64_t *kr = rows + kPolarMaxKernel * j;
                 for (int it = lane; it < tot; it += 64) {
                     const int q = (int)act[it / d], s = it % d;
                     uint8_t *off = Oof(q, j);
@@ -187,10 +360,21 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                         const uint8_t kn = Cof(q, j + 1)[(loc - 1) * d + s];
                         if (kn)
                             for (int i = 0; i < l; ++i)
-                                if ((kr[loc - 1] >> i) & 1u) off[i * d + s] ^= 1u;
+                                if ((kr[loc - 1] >> i) & 1ull) off[i * d + s] ^= 1u;
                     }
                 }
                 wsync();
+                if (p.ml[j]) {
+                    // exact ordered-statistics search (kernels larger than the trellis limit):
+                    // one item at a time, the whole wave on it
+                    for (int it = 0; it < tot; ++it) {
+                        const int q = (int)act[it / d], s = it % d;
+                        const float v = ml_llr(kr, l, loc, Sof(q, j), Oof(q, j), d, s, lane, ms);
+                        if (lane == 0) Sof(q, j + 1)[s] = v;
+                        wsync();
+                    }
+                    continue;
+                }
                 if (p.trellis[j]) {
                     // CTrellisKernelProcessor::GetLLRs (:260-292) as a pull-form Viterbi: a state
                     // of depth dd + 1 takes the smaller of its (at most two) predecessors' metrics,
@@ -264,12 +448,12 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                         s = it % d;
                         const float *src = Sof(q, j);
                         const uint8_t *off = Oof(q, j);
-                        float ay[kPolarMaxKernel];
-                        uint32_t hd = 0;
+                        float ay[kPolarMaxTrellisKernel];  // enumerated layers: l <= 32
+                        uint64_t hd = 0;
                         for (int jj = 0; jj < l; ++jj) {
                             const float v = src[jj * d + s];
                             const float yv = off[jj * d + s] ? -v : v;
-                            if (yv < 0.0f) hd |= 1u << jj;  // HD = Y < 0 (:276)
+                            if (yv < 0.0f) hd |= 1ull << jj;  // HD = Y < 0 (:276)
                             ay[jj] = fabsf(yv);
                         }
                         coset_min(kr, l, loc, ay, hd, (uint32_t)sub, (uint32_t)lpi, b0, b1);
@@ -362,20 +546,17 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                     const uint32_t psi = ph2 / (uint32_t)l;
                     const int next = stride * l;
                     const int phi0 = lam > 1 ? (int)(psi % (uint32_t)p.ksize[lam - 2]) * next : 0;
-                    const uint32_t *kr = rows + kPolarMaxKernel * (lam - 1);
+                    const uint64_t *kr = rows + kPolarMaxKernel * (lam - 1);
                     const int tot = nact * stride;
                     for (int it = lane; it < tot; it += 64) {
                         const int q = (int)act[it / stride], s = it % stride;
                         const uint8_t *x = Cof(q, lam);
                         uint8_t *yo = Cof(q, lam - 1) + phi0;
                         // (y_i) = (x_j) K: y_i = XOR over rows j with K[j][i] (LinAlg.cpp:685-709)
-                        uint32_t xin = 0;
-                        for (int jj = 0; jj < l; ++jj) xin |= (uint32_t)(x[jj * stride + s] & 1u) << jj;
-                        for (int i = 0; i < l; ++i) {
-                            uint32_t acc = 0;
-                            for (int jj = 0; jj < l; ++jj) acc ^= ((xin >> jj) & (kr[jj] >> i)) & 1u;
-                            yo[i * stride + s] = (uint8_t)acc;
-                        }
+                        uint64_t yv = 0;
+                        for (int jj = 0; jj < l; ++jj)
+                            if (x[jj * stride + s] & 1u) yv ^= kr[jj];
+                        for (int i = 0; i < l; ++i) yo[i * stride + s] = (uint8_t)((yv >> i) & 1ull);
                     }
                     wsync();
                     stride = next;

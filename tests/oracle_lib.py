@@ -67,6 +67,10 @@ def lib():
         L.orc_sweep_block.argtypes = [P(OrcCode), C.c_double, C.c_int, C.c_double, C.POINTER(C.c_uint64),
                                       C.c_long, C.c_long, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p]
+        L.orc_sweep_range.argtypes = [P(OrcCode), C.c_double, C.c_int, C.c_double, C.POINTER(C.c_uint64),
+                                      C.c_uint64, C.c_long, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p]
+        L.orc_sweep_range.restype = C.c_long
         _lib = L
     return _lib
 
@@ -149,6 +153,19 @@ class Oracle:
         lib().orc_sweep_block(C.byref(self.code), decoder_snr_db, J, snr_db, C.byref(st), skip, B,
                               _p(tx), _p(res), _p(acc), _p(ops), _p(states))
         return tx, res, acc, ops, states, st.value
+
+    def sweep_range(self, J, snr_db, state, draws, max_words, decoder_snr_db=0.5):
+        """fun()'s loop body over the words of `draws` engine draws (orc_sweep_range)."""
+        tx = np.zeros((max_words, self.n), np.uint8)
+        res = np.zeros((max_words, self.n), np.uint8)
+        acc = np.zeros(max_words, np.uint8)
+        ops = np.zeros((max_words, 3), np.uint64)
+        states = np.zeros(max_words, np.uint64)
+        st = C.c_uint64(state)
+        B = lib().orc_sweep_range(C.byref(self.code), decoder_snr_db, J, snr_db, C.byref(st), draws, max_words,
+                                  _p(tx), _p(res), _p(acc), _p(ops), _p(states))
+        assert B >= 0, "the range does not end on a word boundary"
+        return tx[:B], res[:B], acc[:B], ops[:B], states[:B], st.value
 
     def stream(self, seed, count, snr_db):
         """The reference's fun() input stream: (tx [count,n], y [count,n])."""

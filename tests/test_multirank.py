@@ -111,22 +111,31 @@ def test_rank_streams_are_disjoint_over_every_draw():
 
 
 class OracleSource:
-    """The C oracle's fun() loop body (test infrastructure) as a sweep block source."""
+    """The C oracle's fun() loop body (test infrastructure) as a sweep block source; the
+    resync (where a rank's part starts) is the product's host function under test."""
 
     def __init__(self, m, t, J):
         self.o, self.J = Oracle(m, t), J
+        self.k, self.n = self.o.k, self.o.n
 
     def block(self, snr, state, skip, B):
         return self.o.sweep_block(self.J, snr, state, skip, B)
+
+    def block_range(self, snr, state, draws, max_words):
+        return self.o.sweep_range(self.J, snr, state, draws, max_words)
+
+    def sync(self, k, n, state, offset, limit):
+        return load().stream_sync(k, n, state, offset, limit)
 
 
 def _sweep_worker(rank, world, port, q, m, t, J, p, e, block):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sd = load().sweep_dist
+    stats = {}
     csv = sd.sharded_sweep(OracleSource(m, t, J), (1 << m) - 1, p, e, dist=dist, world=world, rank=rank,
-                           block=block)
-    q.put((rank, csv))
+                           block=block, stats=stats)
+    q.put((rank, csv, stats))
     dist.destroy_process_group()
 
 
@@ -144,31 +153,66 @@ def test_sharded_sweep_equals_reference_csv_cpu(world):
         sd = load().sweep_dist
         assert sd.sharded_sweep(OracleSource(4, 2, -1), 15, 10000, 10000, block=700) == want
         return
-    for _, csv in _run(world, _sweep_worker, 4, 2, -1, 10000, 10000, 700):
+    for _, csv, _ in _run(world, _sweep_worker, 4, 2, -1, 10000, 10000, 700):
         assert csv == want
 
 
 def test_sharded_sweep_error_cut_world2_cpu():
     # BCH(31,16,7), J = inf, p = 10^4, e = 100: the e-th frame error ends most points
     want = _golden("sweep_m5t3_p10000_e100.csv")
-    for _, csv in _run(2, _sweep_worker, 5, 3, -1, 10000, 100, 300):
+    for _, csv, _ in _run(2, _sweep_worker, 5, 3, -1, 10000, 100, 300):
         assert csv == want
 
 
-class GpuSource:
-    def __init__(self, m, t, J):
-        self.d = load().KanekoKernelProcessor(m, t, J=J, device=0)
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", ["sweep_m4t2_p10000_e10000.csv", "sweep_m5t3_p10000_e100.csv"])
+def test_sharded_sweep_resync_parts_equal_reference_csv_cpu(world, name):
+    # large rounds: every rank's part starts at a word start found by bchk_stream_sync (no
+    # parse of the parts before it); same CSV as the reference binary's
+    m, t = (4, 2) if "m4t2" in name else (5, 3)
+    p, e = (10000, 10000) if "m4t2" in name else (10000, 100)
+    want = _golden(name)
+    out = _run(world, _sweep_worker, m, t, -1, p, e, 8192)
+    for _, csv, stats in out:
+        assert csv == want
+        assert stats["ranged_rounds"] > 0
+    # the parts tile each round: the words generated over the ranks ~ the words the sweep used
+    assert sum(st["words"] for _, _, st in out) >= sum(1 for _ in want.splitlines())
 
-    def block(self, snr, state, skip, B):
-        return self.d.sweep_block(snr, state, skip, B)
+
+def test_stream_sync_finds_the_streams_word_starts():
+    # bchk_stream_sync's word start == one of the word boundaries of the sequential stream
+    # (the oracle's draw count, pinned to the reference engine), for random offsets
+    F = load()
+    for m, t in ((4, 2), (5, 3), (6, 6)):
+        o = Oracle(m, t)
+        start = F.rng_jump(1, 987654)
+        bounds, x = [0], start
+        for _ in range(1500):
+            d, x2 = o.stream_draws(x, 1, 2.0)
+            bounds.append(bounds[-1] + d)
+            x = x2
+        assert F.stream_skip(o.k, o.n, start, 1500) == (x, bounds[-1])
+        bset = set(bounds)
+        rng = np.random.default_rng(m)
+        hits = 0
+        for off in rng.integers(1, bounds[-1] // 2, 25):
+            r = F.stream_sync(o.k, o.n, start, int(off), bounds[-1] - int(off))
+            if r is None:
+                continue
+            hits += 1
+            w, st = r
+            assert w >= off and w in bset
+            assert F.stream_skip(o.k, o.n, start, bounds.index(w))[0] == st
+        assert hits >= 20
 
 
 def _gpu_sweep_worker(rank, world, port, q, m, t, J, p, e, block):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    src = GpuSource(m, t, J)
-    csv = load().sweep_dist.sharded_sweep(src, (1 << m) - 1, p, e, dist=dist, world=world, rank=rank,
-                                          block=block)
+    F = load()
+    src = F.sweep_dist.GpuSource(F, m, t, J)
+    csv = F.sweep_dist.sharded_sweep(src, (1 << m) - 1, p, e, dist=dist, world=world, rank=rank, block=block)
     single = src.d.sweep(p, e) if rank == 0 else None
     q.put((rank, csv, single))
     dist.destroy_process_group()

@@ -105,6 +105,8 @@ def _field_order(K, power, prim):
 
 
 KERNELS = {
+    "bch64f": _field_order(_bch_kernel(6, 0b1000011), 6, 0b1000011),  # exact ordered-statistics LLRs
+    "bch64": _bch_kernel(6, 0b1000011),
     "bch8": _bch_kernel(3, 0b1011),
     "bch32f": _field_order(_bch_kernel(5, 0b100101), 5, 0b100101),  # trellis: 2^12 states
     "bch16": _bch_kernel(4, 0b10011),
@@ -169,9 +171,9 @@ def test_spec_errors_before_the_device(kdir, tmp_path):
     (tmp_path / "sing.txt").write_text("3\n1 0 0\n1 0 0\n0 1 1\n")
     (tmp_path / "big.txt").write_text(_kernel_text(_lower_kernel(20, 1)))
     (tmp_path / "wide.txt").write_text(_kernel_text(_lower_kernel(32, 1)))
-    (tmp_path / "huge.txt").write_text("40\n" + "\n".join(" ".join("1" if c <= r else "0" for c in range(40))
-                                                         for r in range(40)) + "\n")
-    for name, msg, n in [("sing", "singular", 3), ("wide", "GPU limit", 32), ("huge", "size", 40),
+    (tmp_path / "huge.txt").write_text("70\n" + "\n".join(" ".join("1" if c <= r else "0" for c in range(70))
+                                                         for r in range(70)) + "\n")
+    for name, msg, n in [("sing", "singular", 3), ("wide", "GPU limit", 32), ("huge", "size", 70),
                          ("missing", "Error reading kernel file", 20)]:
         spec = f"{n} {n // 2} 0 1 0 0\n-{name}.txt\n" + "".join(f"1 {i}\n" for i in range(n - n // 2))
         with pytest.raises(F.BchkError, match=msg):
@@ -245,7 +247,7 @@ def _plr_kernel(K):
     import ctypes as C
 
     class PK(C.Structure):
-        _fields_ = [("size", C.c_int), ("arikan", C.c_int), ("K", C.c_uint8 * 1024), ("Kinv", C.c_uint8 * 1024)]
+        _fields_ = [("size", C.c_int), ("arikan", C.c_int), ("K", C.c_uint8 * 4096), ("Kinv", C.c_uint8 * 4096)]
 
     k = PK()
     k.size, k.arikan = len(K), 0
