@@ -388,25 +388,41 @@ kaneko_fast_kernel(SearchParams p) {
     }
 
     BCHK_STAMP(4)
-    // ---- outputs: resolved rows through LDS, one coalesced 64-row block per wave
+    // ---- outputs: resolved rows through LDS, one coalesced 64-row block per wave. Only the
+    // rows this kernel resolved are written (unresolved ones belong to the exact kernel and
+    // keep the caller's contents): a 16-B chunk all of whose rows are resolved is stored
+    // whole, one that also touches an unresolved row byte by byte (rare).
     const bool resolved = live && state != 0;
+    const uint64_t resm = ballot(resolved);
     uint8_t *out = reinterpret_cast<uint8_t *>(stage);
     const uint64_t x = yH ^ best;
     if (resolved) {
 #pragma unroll
         for (int pos = 0; pos < N; ++pos) out[lane * N + pos] = (uint8_t)((x >> pos) & 1ull);
-    } else if (live) {  // unresolved: keep the caller's row as it is
-        for (int pos = 0; pos < N; ++pos) out[lane * N + pos] = p.res[(size_t)cw * N + pos];
     }
     wave_sync();
+    auto rows_of = [&](int i) {  // rows touched by 16-B chunk i of the block
+        const int r0 = (16 * i) / N, r1 = (16 * i + 15) / N;
+        return ((2ull << (r1 < 63 ? r1 : 63)) - 1ull) & ~((1ull << r0) - 1ull);
+    };
     uint8_t *dst = p.res + (size_t)cw0 * N;
-    if (cw0 + 64u <= p.count && ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0)) {
+    const bool whole = cw0 + 64u <= p.count && ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0);
+    if (whole) {
         const uint4 *src4 = reinterpret_cast<const uint4 *>(out);
         uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
-        for (int i = lane; i < 4 * N; i += 64) dst4[i] = src4[i];
+        for (int i = lane; i < 4 * N; i += 64) {
+            const uint64_t need = rows_of(i);
+            if ((resm & need) == need) {
+                dst4[i] = src4[i];
+            } else if (resm & need) {
+                for (int b = 0; b < 16; ++b)
+                    if ((resm >> ((16 * i + b) / N)) & 1ull) dst[16 * i + b] = out[16 * i + b];
+            }
+        }
     } else {
         const int rows = (int)((p.count - cw0) < 64u ? (p.count - cw0) : 64u);
-        for (int i = lane; i < rows * N; i += 64) dst[i] = out[i];
+        for (int i = lane; i < rows * N; i += 64)
+            if ((resm >> (i / N)) & 1ull) dst[i] = out[i];
     }
     if (p.cnt) {
         // fused counters (src/dataForPlot.cpp:55-74) of the resolved rows: the sent words'
@@ -415,24 +431,28 @@ kaneko_fast_kernel(SearchParams p) {
         rowerr[lane] = 0u;
         wave_sync();
         const uint8_t *txb = p.tx + (size_t)cw0 * N;
-        if (cw0 + 64u <= p.count && ((reinterpret_cast<uintptr_t>(txb) & 15u) == 0)) {
+        if (whole && ((reinterpret_cast<uintptr_t>(txb) & 15u) == 0)) {
             const uint4 *a4 = reinterpret_cast<const uint4 *>(txb);
             const uint4 *b4 = reinterpret_cast<const uint4 *>(out);
             for (int v = lane; v < 4 * N; v += 64) {
+                const uint64_t need = rows_of(v);
+                if (!(resm & need)) continue;  // no resolved row in this chunk
                 const uint4 a = a4[v], b = b4[v];
                 const uint32_t xx[4] = {a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     if (!xx[k]) continue;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if ((xx[k] >> (8 * q)) & 0xFFu) atomicAdd(&rowerr[(16 * v + 4 * k + q) / N], 1u);
+                    for (int q = 0; q < 4; ++q) {
+                        const int row = (16 * v + 4 * k + q) / N;
+                        if (((xx[k] >> (8 * q)) & 0xFFu) && ((resm >> row) & 1ull)) atomicAdd(&rowerr[row], 1u);
+                    }
                 }
             }
         } else {
             const int rows = (int)((p.count - cw0) < 64u ? (p.count - cw0) : 64u);
             for (int i = lane; i < rows * N; i += 64)
-                if (txb[i] != out[i]) atomicAdd(&rowerr[i / N], 1u);
+                if (((resm >> (i / N)) & 1ull) && txb[i] != out[i]) atomicAdd(&rowerr[i / N], 1u);
         }
         wave_sync();
         const uint32_t e = resolved ? rowerr[lane] : 0u;

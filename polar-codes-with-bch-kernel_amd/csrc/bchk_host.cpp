@@ -402,6 +402,9 @@ struct bchk_ctx {
     uint64_t last_tail_stats[6] = {0, 0, 0, 0, 0, 0};
     bool tail_diag_on = false;     // BCHK_TAIL_DIAG=1: per-codeword tail timing records
     bool tail_concurrent = false;  // BCHK_TAIL_CONCURRENT=1: the tail kernel beside the first pass
+    // BCHK_TAIL_INLINE=1: the first pass IS the analytic-tail kernel instance -- a codeword
+    // past the chunk limit is finished by the same wave at once, no second kernel
+    bool tail_inline = false;
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
     // hybrid tail: a first-pass hand-off whose loop bound is below this goes to a cooperative
@@ -573,7 +576,13 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
     const int grid_coop = tabk ? c->grid_coop_tab : c->grid_coop;
     // analytic tail: the first pass hands its heavy codewords to the tail kernel (queue
     // l1q), which finishes most of them and hands the rest to the cooperative kernel
-    const bool tail = c->analytic && c->ks.tail && p.heavy_tail && variant == BCHK_VARIANT_ANSWER;
+    // n <= 31 without a pattern cap below n: every position is a flip position (NB = n), so
+    // the kernel of the flip columns has the code's dimension k > 3 and an_plan hands every
+    // codeword on -- straight to the cooperative kernel instead (same results, no wasted pass)
+    const bool an_useless = c->n <= 31 && (c->J < 0 || c->J >= c->n) && c->k > 3;
+    const bool tail_any = c->analytic && c->ks.tail && p.heavy_tail && variant == BCHK_VARIANT_ANSWER && !an_useless;
+    const bool inl = tail_any && c->tail_inline && !c->tail_diag_on;  // the first pass finishes its tails
+    const bool tail = tail_any && !inl;
     if (tail && (rc = P.l1rec.ensure(B * sizeof(TailRec)))) return rc;
     if (tail && B > P.l1q.cap / sizeof(uint32_t)) {
         if ((rc = P.l1q.ensure(B * sizeof(uint32_t)))) return rc;
@@ -623,16 +632,22 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             q.heavy_big = hybrid ? c->tail_min_bound : 0;
             q.tail_rec = (TailRec *)P.l1rec.p;
         }
+        if (inl) {  // the analytic tail inside the first pass; failures to the cooperative kernel
+            q.analytic = 1;
+            q.tail_stats = ctrl + kTailStats;
+        }
+        const int igrid = tabk ? c->grid_tail_tab : c->grid_tail;
         if (fast) {
             q.queue = (const uint32_t *)P.queue.p;
             q.qcount = ctrl;
             q.heads = ctrl + 32;
             if (c->heavy_first && c->m <= 6) q.qfront_n = ctrl + kQFront;
             // every resident wave may take work; waves beyond the queue length exit at once
-            HIP_TRY(launch_search(c->ks, q, grid, c->lds, s));
+            HIP_TRY(inl ? launch_tail(c->ks, q, igrid, c->lds_tail, s) : launch_search(c->ks, q, grid, c->lds, s));
         } else {
             const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
-            HIP_TRY(launch_search(c->ks, q, std::max(1, std::min(grid, need)), c->lds, s));
+            HIP_TRY(inl ? launch_tail(c->ks, q, std::max(1, std::min(igrid, need)), c->lds_tail, s)
+                        : launch_search(c->ks, q, std::max(1, std::min(grid, need)), c->lds, s));
         }
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[3], s));
@@ -818,6 +833,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (getenv("BCHK_NO_ANALYTIC")) c->analytic = false;
     if (getenv("BCHK_TAIL_DIAG")) c->tail_diag_on = true;
     if (const char *tc = getenv("BCHK_TAIL_CONCURRENT")) c->tail_concurrent = atoi(tc) != 0;
+    if (const char *ti = getenv("BCHK_TAIL_INLINE")) c->tail_inline = atoi(ti) != 0;
     if (const char *tb = getenv("BCHK_TAIL_BLOCKS")) c->tail_conc_blocks = std::max(1, atoi(tb));
     if (const char *tm = getenv("BCHK_TAIL_MIN_BOUND")) c->tail_min_bound = strtoull(tm, nullptr, 10);
     if (const char *hf = getenv("BCHK_HEAVY_FIRST")) c->heavy_first = atoi(hf) != 0;

@@ -39,7 +39,7 @@ for layers, K, L, B, tmin in CASES:
     g = time.perf_counter() - t0
     n_cpu = 32 if o.U <= 256 else 8
     t0 = time.perf_counter()
-    want = o.decode_batch(llr[:n_cpu], L)
+    want = o.decode_batch(llr[:n_cpu], L, threads=1)
     c = time.perf_counter() - t0
     same = all(np.array_equal(a[:n_cpu], b) for a, b in zip(got, want))
     print(json.dumps({"layers": "-".join(layers), "U": o.U, "K": K, "L": L, "B": B, "trellis_min_size": tmin,

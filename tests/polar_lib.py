@@ -86,14 +86,23 @@ class PolarOracle:
         assert n >= 1
         return n, info, cw, met
 
-    def decode_batch(self, llrs, L):
+    def decode_batch(self, llrs, L, threads=None):
+        """Rows decoded independently, over host threads (plr_decode keeps no global state;
+        ctypes releases the GIL during the call)."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle_lib import host_threads
         B = llrs.shape[0]
         cnt = np.zeros(B, np.int32)
         info = np.zeros((B, L, self.K), np.uint8)
         cw = np.zeros((B, L, self.N), np.uint8)
         met = np.zeros((B, L), np.float32)
-        for b in range(B):
+
+        def one(b):
             cnt[b], info[b], cw[b], met[b] = self.decode(llrs[b], L)
+
+        with ThreadPoolExecutor(max_workers=min(threads or host_threads(), max(1, B))) as ex:
+            list(ex.map(one, range(B)))
         return cnt, info, cw, met
 
 

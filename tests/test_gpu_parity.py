@@ -17,7 +17,7 @@ _ctx = {}
 
 # execution paths, all of which must give the reference's results:
 #   "fast+exact+tail"  default: lane-per-codeword fast path, wave-per-codeword exact kernel,
-#                      after 2 chunks the analytic tail kernel (candidate codewords,
+#                      after 8 chunks (chunk_limit) the analytic tail kernel (candidate codewords,
 #                      csrc/bchk_kernels.hip), the cooperative kernel for what it hands on
 #   "exact-only"       no fast path, no hand-off (one wave per codeword, every pattern)
 #   "tail-early"       analytic tail after the first chunk
