@@ -483,8 +483,15 @@ static float enum_minsum_llr(const plr_kernel *k, int phase, const float *y) {
  * disagree), so a depth-first search over E, cheapest pivot first, pruning every subtree whose
  * flip cost exceeds the best metric found (less a float-rounding margin), visits every word
  * that can be the minimum: the value is the enumeration's. */
-static __thread long ml_nodes_last;
+static __thread long ml_nodes_last, ml_nodes_total, ml_calls_total;
 long plr_ml_nodes(void) { return ml_nodes_last; }
+/* totals over this thread's searches since the last call (diagnostics) */
+long plr_ml_nodes_total(long *calls) {
+    const long t = ml_nodes_total;
+    if (calls) *calls = ml_calls_total;
+    ml_nodes_total = ml_calls_total = 0;
+    return t;
+}
 
 static float ml_minsum_llr(const plr_kernel *k, int phase, const float *y) {
     const int l = k->size, nf = l - phase - 1;
@@ -521,6 +528,13 @@ static float ml_minsum_llr(const plr_kernel *k, int phase, const float *y) {
     /* a float sum of at most 64 non-negative terms is within 64 u (u = 2^-24) of the exact
      * sum: a subtree is pruned only when its exact cost exceeds best by more than that */
     const double shrink = 1.0 - 1.0 / 32768.0;
+    /* U[i]: the non-pivot positions rows po[i..] can still change; below a word that has
+     * taken pivots up to po[i - 1], every other non-pivot disagreement is fixed */
+    uint64_t pivm = 0, U[PLR_MAXKERNEL + 1];
+    for (int i = 0; i < nf; ++i) pivm |= 1ull << piv[i];
+    const uint64_t lrb = ~pivm & (l == 64 ? ~0ull : ((1ull << l) - 1));
+    U[nf] = 0;
+    for (int i = nf - 1; i >= 0; --i) U[i] = U[i + 1] | (G[po[i]] & lrb);
     float best[2];
     typedef struct { uint64_t c; double lb; int i; } node;
     node *st = malloc(sizeof(node) * (size_t)(nf + 2));
@@ -540,6 +554,9 @@ static float ml_minsum_llr(const plr_kernel *k, int phase, const float *y) {
                 const double lb2 = n.lb + ay[piv[po[i]]];
                 if (lb2 * shrink > best[b]) break; /* costs increase with i */
                 const uint64_t c2 = n.c ^ G[po[i]];
+                /* c2 and everything below it disagree at least at its fixed non-pivot positions */
+                const double fx = word_metric((c2 ^ hd) & lrb & ~U[i + 1], ay, l);
+                if ((lb2 + fx) * shrink > best[b]) continue;
                 const float m = word_metric(c2 ^ hd, ay, l);
                 ++nodes;
                 if (m < best[b]) best[b] = m;
@@ -549,6 +566,8 @@ static float ml_minsum_llr(const plr_kernel *k, int phase, const float *y) {
     }
     free(st);
     ml_nodes_last = nodes;
+    ml_nodes_total += nodes;
+    ++ml_calls_total;
     return best[1] - best[0]; /* :292 */
 }
 

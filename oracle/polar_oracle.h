@@ -63,5 +63,7 @@ float plr_minsum_llr(const plr_kernel *k, int phase, const float *y);
 float plr_minsum_llr_by(const plr_kernel *k, int phase, const float *y, int method);
 /* nodes (candidate codewords) the last PLR_BY_ML call of this thread evaluated */
 long plr_ml_nodes(void);
+/* nodes and searches of this thread since the previous call (then reset) */
+long plr_ml_nodes_total(long *calls);
 
 #endif

@@ -576,11 +576,9 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
     const int grid_coop = tabk ? c->grid_coop_tab : c->grid_coop;
     // analytic tail: the first pass hands its heavy codewords to the tail kernel (queue
     // l1q), which finishes most of them and hands the rest to the cooperative kernel
-    // n <= 31 without a pattern cap below n: every position is a flip position (NB = n), so
-    // the kernel of the flip columns has the code's dimension k > 3 and an_plan hands every
-    // codeword on -- straight to the cooperative kernel instead (same results, no wasted pass)
-    const bool an_useless = c->n <= 31 && (c->J < 0 || c->J >= c->n) && c->k > 3;
-    const bool tail_any = c->analytic && c->ks.tail && p.heavy_tail && variant == BCHK_VARIANT_ANSWER && !an_useless;
+    // (n <= 31 without a pattern cap below n: every position is a flip position, and the
+    // analytic tail lists the improving codewords by an ordered-statistics search, an_osd)
+    const bool tail_any = c->analytic && c->ks.tail && p.heavy_tail && variant == BCHK_VARIANT_ANSWER;
     const bool inl = tail_any && c->tail_inline && !c->tail_diag_on;  // the first pass finishes its tails
     const bool tail = tail_any && !inl;
     if (tail && (rc = P.l1rec.ensure(B * sizeof(TailRec)))) return rc;

@@ -877,6 +877,164 @@ __device__ __forceinline__ uint64_t an_earliest(const AnWave *A, double lim, int
     return best == 0xFFFFFFFFu ? ~0ull : (((uint64_t)best + 63ull) & ~63ull);
 }
 
+// Candidates of a code with n <= 31 when every position can be flipped by some pattern (the
+// loop bound uncapped, or no improvement yet: NB = n). The flip columns' kernel then has the
+// code's dimension, too large for an_enumerate; instead the codewords that can still
+// improve l0 are listed directly by an ordered-statistics search. Gauss-Jordan over the
+// syndrome bits (one column per lane, lane = reliability rank, lane n the hard decision's
+// syndrome) picks pivot columns (least reliable first); every other rank j then has a
+// representation comb_j over the pivots (its own bit included) and S0 has comb0, so the
+// codewords are c = yH ^ D with D = comb0 ^ XOR_{j in E} comb_j over the sets E of non-pivot
+// ranks. D includes E, so l(c) >= sum_E a: a depth-first search over E (non-pivot ranks in
+// ascending reliability, 64 nodes per step from a LIFO in the wave's stack) that drops a
+// subtree once that sum exceeds l0 lists every codeword with l(c) < l0. Each one's first
+// pattern is D (as rank bits) with its t highest bits cleared (1 when D = 0: the hard
+// decision is a codeword and pattern 0 fails on it), as an_emit. The candidates then go to
+// an_replay exactly as an_enumerate's. Returns 0, or 1 budget / 2 stack / 3 list full.
+template <int M, int TMAX>
+__device__ int an_osd(const SearchState<1> &S, const Prep<M, TMAX> &P, AnWave *A, const uint32_t *col,
+                      const uint8_t *ordl, const double *ap, uint64_t ifrom, uint64_t BM, int t, int lane,
+                      uint32_t &iters) {
+    constexpr int N = Geo<M>::N, W = Prep<M, TMAX>::W;
+    static_assert(N <= 31, "rank masks are 32-bit");
+    uint64_t v = 0;
+    if (lane < N) {
+        const int pos = P.ordv[0];
+#pragma unroll
+        for (int w = 0; w < W; ++w) v |= (uint64_t)col[pos * W + w] << (32 * w);
+    } else if (lane == N) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) v |= (uint64_t)P.S0[w] << (32 * w);
+    }
+    uint32_t comb = lane < N ? (1u << lane) : 0u;
+    bool used = false;
+#pragma unroll
+    for (int q = 0; q < TMAX; ++q) {
+        if (q >= t) break;
+#pragma unroll
+        for (int b = 0; b < M; ++b) {
+            const int bit = 8 * q + b;
+            const bool has = (v >> bit) & 1ull;
+            const uint64_t cm = ballot(has && lane < N && !used);
+            if (!cm) continue;
+            const int k = (int)__builtin_ctzll(cm);
+            const uint64_t pv = rdl64(v, k);
+            const uint32_t pc = rdl(comb, k);
+            if (has && lane != k) {
+                v ^= pv;
+                comb ^= pc;
+            }
+            used = used || lane == k;
+        }
+    }
+    const uint32_t comb0 = rdl(comb, N);
+    const uint64_t freem = ballot(lane < N && !used);  // non-pivot ranks, ascending reliability
+    const int nf = __popcll(freem);
+    const double a_me = P.asv[0];                       // a of rank `lane`
+    // per free index f (ascending rank): its comb and cost, through the stack's spare words
+    uint32_t *fcomb = reinterpret_cast<uint32_t *>(A->cmask);  // 32 entries: nf <= 31
+    double *fcost = reinterpret_cast<double *>(A->dsum);      // 128 entries
+    if (lane < N && !used) {
+        const int f = __popcll(freem & ((1ull << lane) - 1ull));
+        fcomb[f] = comb;
+        fcost[f] = a_me;
+    }
+    if (lane == 0) A->ncand = 0u;
+    wave_sync();
+    const double lim = S.l0 * (1.0 + 0x1p-40);  // sums of <= 31 terms in another order
+    const double l0 = S.l0;
+    // a codeword D (rank bits): its candidate record when it can improve l0
+    auto consider = [&](bool live, uint32_t D) {
+        uint64_t Dp = 0;
+        double l = 0.0;
+        uint32_t ifirst = 0;
+        bool ok = live;
+        if (live) {
+            for (uint32_t x = D; x; x &= x - 1) Dp |= 1ull << ordl[__builtin_ctz(x)];
+            for (uint64_t x = Dp; x; x &= x - 1) l += ap[__builtin_ctzll(x)];  // calcL, index order
+            if (__popc(D) <= t) {
+                ifirst = D == 0u ? 1u : 0u;
+            } else {
+                uint32_t x = D;
+                for (int k = 0; k < t; ++k) x &= ~(1u << (31 - __builtin_clz(x)));
+                ifirst = x;
+            }
+            ok = l < l0 && (uint64_t)ifirst >= ifrom && (uint64_t)ifirst < BM;
+        }
+        if (ok) {
+            const uint32_t slot = atomicAdd(&A->ncand, 1u);
+            if (slot < (uint32_t)kAnCand) {
+                AnCand c;
+                c.D = Dp;
+                c.l = l;
+                c.i = ifirst;
+                c.m = (uint32_t)__popcll(Dp);
+                A->cand[slot] = c;
+            }
+        }
+    };
+    consider(lane == 0, comb0);  // E empty
+    // nodes: the words D ^ fcomb[f] (f = next) and below them; lb = cost of E so far
+    int sp = 0;
+    if (nf > 0 && lane == 0) {
+        AnNode r;
+        r.rem = comb0;
+        r.sum = __double_as_longlong(0.0);
+        r.sel = 0;
+        r.comb = 0;
+        r.next = 0;
+        r.pad = 0;
+        A->stack[0] = r;
+    }
+    sp = nf > 0 ? 1 : 0;
+    wave_sync();
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t steps = 0;
+    while (sp > 0) {
+        int n = sp < 64 ? sp : 64;
+        const int room = kAnStack - 64 - sp;
+        if (room < n) n = room > 1 ? room : 1;
+        const bool have = lane < n;
+        AnNode e;
+        e.rem = 0;
+        e.sum = 0;
+        e.next = 0;
+        if (have) e = A->stack[sp - n + lane];
+        sp -= n;
+        wave_sync();
+        const int f = (int)e.next;
+        const double lb = __longlong_as_double(e.sum);
+        const double lb2 = have ? lb + fcost[f] : 0.0;
+        const bool live = have && lb2 <= lim;
+        const uint32_t D2 = (uint32_t)e.rem ^ fcomb[f < 31 ? f : 0];
+        consider(live, D2);
+        const bool more = live && f + 1 < nf;
+        const double nc = more ? fcost[f + 1] : 0.0;
+        const bool psib = more && lb + nc <= lim;
+        const bool pch = more && lb2 + nc <= lim;
+        const uint64_t ms = ballot(psib), mc = ballot(pch);
+        const int nsib = __popcll(ms);
+        if (sp + nsib + __popcll(mc) > kAnStack) return 2;
+        if (psib) {
+            AnNode c = e;
+            c.next = (uint32_t)(f + 1);
+            A->stack[sp + __popcll(ms & below)] = c;
+        }
+        if (pch) {
+            AnNode c = e;
+            c.rem = D2;
+            c.sum = __double_as_longlong(lb2);
+            c.next = (uint32_t)(f + 1);
+            A->stack[sp + nsib + __popcll(mc & below)] = c;
+        }
+        sp += nsib + __popcll(mc);
+        wave_sync();
+        ++iters;
+        if (++steps > 4096u) return 1;
+    }
+    return A->ncand <= (uint32_t)kAnCand ? 0 : 3;
+}
+
 struct AnPlan {
     int mode;       // 0: hand off, 1: candidates complete from ifrom, 2: exact below stop
     uint64_t stop;  // mode 2: first pattern the replay takes over (a chunk boundary)
@@ -906,6 +1064,18 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     uint64_t BM;  // patterns at or past BM are never processed
     if (S.impr == 0) BM = S.bound;
     else BM = (J >= 0 && J < 31) ? (1ull << J) - 1ull : 0x7FFFFFFFull;
+    if constexpr (N <= 31) {
+        if (NB >= N) {  // every position flippable: list the improving codewords directly
+            const int er = an_osd<M, TMAX>(S, P, A, col, ordl, ap, ifrom, BM, t, lane, iters);
+            if (!er) {
+                plan.mode = 1;
+                return plan;
+            }
+            plan.fails |= 1 << er;
+            plan.why = 2;
+            return plan;
+        }
+    }
     if (NB < 31 && BM > (1ull << NB)) { plan.why = 1; return plan; }
     // Gaussian elimination over GF(2), one column per lane: lanes r < NB the flip columns
     // (rank r), NB <= r < N the U columns, lane N the hard decision's syndrome S0

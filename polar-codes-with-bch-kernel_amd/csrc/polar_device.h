@@ -43,11 +43,12 @@ constexpr int kPolarMaxMatrixGpu = 64;  // the 2^6 extended-BCH kernel (CTrellis
 constexpr int kPolarMaxTrellisKernel = 32;  // the trellis is built for kernels up to 32 only
 // Matrix layers of size > 32 (or from BCHK_POLAR_ML up) take their LLRs from an exact
 // ordered-statistics search instead (one wave per item, polar_mixed.hip ml_llr): per wave an
-// LDS scratch of kMlStack 16-byte search nodes, the reduced basis (64 u64), flip costs and
-// |y| (64 floats each). Phases whose coset has at most 2^kMlEnumBits words are enumerated.
-constexpr int kMlStack = 2048;
+// LDS scratch of kMlStack 12-byte search nodes, the reduced basis and the suffix unions of its
+// non-pivot parts (64 + 65 u64), flip costs and |y| (64 floats each). Phases whose coset has
+// at most 2^kMlEnumBits words are enumerated.
+constexpr int kMlStack = 1536;
 constexpr int kMlEnumBits = 10;
-constexpr uint32_t kMlScratchBytes = 16u * kMlStack + 8u * 64u + 4u * 64u + 4u * 64u;
+constexpr uint32_t kMlScratchBytes = 12u * kMlStack + 8u * 64u + 8u * 65u + 8u + 4u * 64u + 4u * 64u;
 // Matrix layers of size >= the trellis threshold (default 16, BCHK_POLAR_TRELLIS) take their
 // LLRs from CTrellisKernelProcessor's trellis (pull-form Viterbi over predecessor lists);
 // smaller ones enumerate the coset (2^(size - 1 - phase) words per LLR). Per (layer, phase):

@@ -103,13 +103,16 @@ __device__ __forceinline__ void coset_min(const uint64_t *rows, int l, int phase
 // can be a minimum: the result is the coset enumeration's, bit for bit. The wave works on one
 // item: 64 lanes sort the positions and eliminate (a lane per row), then evaluate 64 search
 // nodes per round (a node per lane) from a LIFO in LDS.
-struct MlNode {  // the words c ^ Gs[i] (and below them): flip cost so far lb, half b
-    uint64_t c;
-    float lb;
-    uint16_t i, b;
-};
+struct MlNode {  // the words c ^ G[i] (and below them): flip cost so far lb, half b
+    uint32_t clo, chi;
+    uint32_t lbib;  // lb's float bits with the low 7 mantissa bits replaced by i << 1 | b
+};                  // (truncating a non-negative float lowers it: still a lower bound)
+__device__ __forceinline__ MlNode ml_node(uint64_t c, float lb, int i, int b) {
+    return MlNode{(uint32_t)c, (uint32_t)(c >> 32), (__float_as_uint(lb) & ~0x7Fu) | ((uint32_t)i << 1) | (uint32_t)b};
+}
 struct MlScratch {
     uint64_t *G;   // [64] reduced basis, by increasing flip cost
+    uint64_t *U;   // [65] U[i]: non-pivot positions rows i.. can change (suffix unions)
     float *cost;   // [64] flip cost of each basis row (|y| at its pivot)
     float *ay;     // [64] |y| by position
     MlNode *stk;   // [kMlStack]
@@ -141,6 +144,16 @@ __device__ __forceinline__ float ml_metric(uint64_t dis, const float *ay, int l)
     float m = 0.0f;
     for (int j = 0; j < l; ++j) m += ((dis >> j) & 1ull) ? ay[j] : 0.0f;
     return m;
+}
+// the same, and (fx) the sum over the subset fix of dis, in one pass
+__device__ __forceinline__ void ml_metric2(uint64_t dis, uint64_t fix, const float *ay, int l, float &m, float &fx) {
+    m = 0.0f;
+    fx = 0.0f;
+    for (int j = 0; j < l; ++j) {
+        const float a = ay[j];
+        m += ((dis >> j) & 1ull) ? a : 0.0f;
+        fx += ((fix >> j) & 1ull) ? a : 0.0f;
+    }
 }
 
 __device__ float ml_llr(const uint64_t *kr, int l, int loc, const float *src, const uint8_t *off, int d, int s,
@@ -204,6 +217,17 @@ __device__ float ml_llr(const uint64_t *kr, int l, int loc, const float *src, co
         ms.G[nf - 1 - t] = g;
         ms.cost[nf - 1 - t] = ms.ay[piv];
     }
+    // non-pivot positions; below a word that has taken rows up to i - 1, every non-pivot
+    // disagreement outside U[i] is fixed, so its |y| bounds the subtree from below too
+    uint64_t pm = lane < nf ? (1ull << piv) : 0ull;
+    for (int o = 1; o < 64; o <<= 1) pm |= shfl_xor64(pm, o);
+    const uint64_t lrb = ~pm & (l >= 64 ? ~0ull : ((1ull << l) - 1ull));
+    wsync();
+    if (lane <= nf) {
+        uint64_t u = 0ull;
+        for (int q = lane; q < nf; ++q) u |= ms.G[q] & lrb;
+        ms.U[lane] = u;
+    }
     // the roots: the word of each half that matches the hard decision on the pivots
     const uint64_t root0 = wave_xor64(lane < nf && ((hd >> piv) & 1ull) ? g : 0ull);
     const uint64_t t1 = hd ^ kr[loc];
@@ -211,8 +235,8 @@ __device__ float ml_llr(const uint64_t *kr, int l, int loc, const float *src, co
     float best0 = ml_metric(root0 ^ hd, ms.ay, l), best1 = ml_metric(root1 ^ hd, ms.ay, l);
     int sp = 0;
     if (lane == 0) {
-        ms.stk[0] = MlNode{root0, 0.0f, 0, 0};
-        ms.stk[1] = MlNode{root1, 0.0f, 0, 1};
+        ms.stk[0] = ml_node(root0, 0.0f, 0, 0);
+        ms.stk[1] = ml_node(root1, 0.0f, 0, 1);
     }
     sp = 2;
     wsync();
@@ -226,20 +250,23 @@ __device__ float ml_llr(const uint64_t *kr, int l, int loc, const float *src, co
         const int room = kMlStack - 128 - sp;
         if (room < n) n = room > 1 ? room : 1;
         const bool have = lane < n;
-        MlNode e{0ull, 0.0f, 0, 0};
+        MlNode e{0u, 0u, 0u};
         if (have) e = ms.stk[sp - n + lane];
         sp -= n;
         wsync();
-        const int i = e.i;
-        const bool hb = e.b != 0;
+        const uint64_t ec = (uint64_t)e.clo | ((uint64_t)e.chi << 32);
+        const float elb = __uint_as_float(e.lbib & ~0x7Fu);
+        const int i = (int)((e.lbib >> 1) & 63u);
+        const bool hb = (e.lbib & 1u) != 0;
         const float bound = hb ? best1 : best0;
-        const float l2 = have ? e.lb + ms.cost[i] : kInf;
+        const float l2 = have ? elb + ms.cost[i] : kInf;
         const bool live = have && l2 * kMlShrink <= bound;
         uint64_t c2 = 0ull;
-        float m = kInf;
+        float m = kInf, fx = 0.0f;
         if (live) {
-            c2 = e.c ^ ms.G[i];
-            m = ml_metric(c2 ^ hd, ms.ay, l);
+            c2 = ec ^ ms.G[i];
+            const uint64_t dis = c2 ^ hd;
+            ml_metric2(dis, dis & lrb & ~ms.U[i + 1], ms.ay, l, m, fx);
         }
         const float n0 = wave_minf(live && !hb ? m : kInf), n1 = wave_minf(live && hb ? m : kInf);
         best0 = n0 < best0 ? n0 : best0;
@@ -247,12 +274,12 @@ __device__ float ml_llr(const uint64_t *kr, int l, int loc, const float *src, co
         const float nb = hb ? best1 : best0;
         const bool more = live && i + 1 < nf;
         const float nc = more ? ms.cost[i + 1] : 0.0f;
-        const bool psib = more && (e.lb + nc) * kMlShrink <= nb;  // the next pivot instead of this one
-        const bool pch = more && (l2 + nc) * kMlShrink <= nb;     // this one and a later one
+        const bool psib = more && (elb + nc) * kMlShrink <= nb;     // the next pivot instead of this one
+        const bool pch = more && (l2 + fx + nc) * kMlShrink <= nb;  // this one and a later one
         const uint64_t ms_ = __ballot(psib), mc = __ballot(pch);
         const int nsib = __builtin_popcountll(ms_);
-        if (psib) ms.stk[sp + __builtin_popcountll(ms_ & lt)] = MlNode{e.c, e.lb, (uint16_t)(i + 1), e.b};
-        if (pch) ms.stk[sp + nsib + __builtin_popcountll(mc & lt)] = MlNode{c2, l2, (uint16_t)(i + 1), e.b};
+        if (psib) ms.stk[sp + __builtin_popcountll(ms_ & lt)] = ml_node(ec, elb, i + 1, hb ? 1 : 0);
+        if (pch) ms.stk[sp + nsib + __builtin_popcountll(mc & lt)] = ml_node(c2, l2, i + 1, hb ? 1 : 0);
         sp += nsib + __builtin_popcountll(mc);
         wsync();
     }
@@ -284,8 +311,9 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
     uint32_t *rec = act + L;
     float *tmet = reinterpret_cast<float *>(smem + o_tm);  // trellis state metrics, 2 x tstates
     uint8_t *mls = smem + ((o_tm + 8 * p.tstates + 15) & ~15);  // ordered-statistics search scratch
-    MlScratch ms{reinterpret_cast<uint64_t *>(mls), reinterpret_cast<float *>(mls + 512),
-                 reinterpret_cast<float *>(mls + 768), reinterpret_cast<MlNode *>(mls + 1024)};
+    MlScratch ms{reinterpret_cast<uint64_t *>(mls), reinterpret_cast<uint64_t *>(mls + 512),
+                 reinterpret_cast<float *>(mls + 1040), reinterpret_cast<float *>(mls + 1296),
+                 reinterpret_cast<MlNode *>(mls + 1552)};
     const bool mine = lane < L;
     for (int i = lane; i < U; i += 64) ph[i] = p.phase[i];
     for (int i = lane; i < kPolarMaxKernel * nl; i += 64) rows[i] = p.krows[i];

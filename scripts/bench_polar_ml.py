@@ -23,7 +23,7 @@ for name, K in KERNELS.items():
     open(os.path.join(kdir, f"{name}.txt"), "w").write(_kernel_text(K))
 B = int(os.environ.get("BENCH_B", "16384"))
 CASES = [(("bch64f",), 32, 8, 2.0), (("bch64f",), 32, 8, 3.0), (("bch64f",), 32, 1, 3.0), (("bch64f",), 32, 4, 3.0),
-         (("A", "bch64f"), 64, 8, 2.5), (("bch64f", "A"), 64, 8, 2.5), (("A", "A", "bch64f"), 128, 8, 2.0)]
+         (("A", "bch64f"), 64, 8, 2.5), (("bch64f", "A"), 64, 8, 2.5)]
 for layers, K, L, snr in CASES:
     spec = mixed_spec(layers, K, dyn=0, seed=1)
     o = PolarOracle(spec, kdir)

@@ -523,3 +523,30 @@ def test_fast_selection_equals_full_sort_with_far_ties(snr):
     acc = a2.astype(bool)
     np.testing.assert_array_equal(r1[idx][acc], r2[acc])
     np.testing.assert_array_equal(l0b[idx][acc].view(np.uint64), l2[acc].view(np.uint64))
+
+
+@pytest.mark.parametrize("m,t,J,snr", [(5, 3, -1, 2.0), (5, 3, -1, 3.0), (5, 3, 15, 1.0), (4, 2, -1, 1.0),
+                                       (5, 2, -1, 2.0)])
+def test_small_code_uncapped_tail_lists_codewords(m, t, J, snr):
+    # n <= 31 with every position flippable (J = inf, or no improvement yet): the analytic tail
+    # lists the improving codewords by an ordered-statistics search (an_osd) -- same rows, l0
+    # bits and counters as the cooperative kernel alone, and the oracle on the heavy rows
+    F = load()
+    on, off = dec(m, t, J=J), dec(m, t, J=J, path="coop-heavy")
+    _, y, _ = on.generate(snr, 1 << 16, seed=606)
+    on.set_max_decodes(1 << 24)
+    off.set_max_decodes(1 << 24)
+    a, b = on.decode(y), off.decode(y)
+    on.set_max_decodes(0)
+    off.set_max_decodes(0)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+    np.testing.assert_array_equal(a[2], b[2])
+    assert not np.any(a[2]["flags"] & F.F_TRUNCATED)
+    st = on.tail_stats()
+    assert on.tail_count() > 0 and st[1] > 0  # codewords finished from the listed candidates
+    heavy = np.flatnonzero(a[2]["decodes"] > 2 + 8 * 64)
+    rows = np.random.default_rng(4).choice(heavy, min(200, len(heavy)), replace=False)
+    o = Oracle(m, t)
+    r2, l2, s2, a2 = o.kaneko_batch(y[rows], J=J)
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, a[0][rows], a[1][rows], a[2][rows])

@@ -128,13 +128,13 @@ class OracleSource:
         return load().stream_sync(k, n, state, offset, limit)
 
 
-def _sweep_worker(rank, world, port, q, m, t, J, p, e, block):
+def _sweep_worker(rank, world, port, q, m, t, J, p, e, block, seed=1, max_snr=5.0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sd = load().sweep_dist
     stats = {}
     csv = sd.sharded_sweep(OracleSource(m, t, J), (1 << m) - 1, p, e, dist=dist, world=world, rank=rank,
-                           block=block, stats=stats)
+                           block=block, stats=stats, seed=seed, max_snr=max_snr)
     q.put((rank, csv, stats))
     dist.destroy_process_group()
 
@@ -178,6 +178,25 @@ def test_sharded_sweep_resync_parts_equal_reference_csv_cpu(world, name):
         assert stats["ranged_rounds"] > 0
     # the parts tile each round: the words generated over the ranks ~ the words the sweep used
     assert sum(st["words"] for _, _, st in out) >= sum(1 for _ in want.splitlines())
+
+
+# draws (from seed 1) whose engine value makes uniform_int_distribution redraw: 16807^d =
+# 2^31 - 3 and 2^31 - 2 (discrete logarithms); the only two in the engine's period
+REDRAW_DRAWS = (311731497, 1073741823)
+
+
+@pytest.mark.parametrize("special", REDRAW_DRAWS)
+def test_sharded_sweep_across_a_redrawn_information_bit_cpu(special):
+    # a sweep whose stream passes one of the two redrawn information draws: the rounds around
+    # it cannot resolve their parts and fall back together; CSV == the single-process sweep
+    F = load()
+    o = Oracle(4, 2)
+    start = F.rng_jump(1, special - 3000 * 60)  # ~3000 BCH(15,7) words before it (~60 draws each)
+    want = o.sweep(20000, 20000, J=-1, max_snr=0.5, seed=start)
+    out = _run(2, _sweep_worker, 4, 2, -1, 20000, 20000, 4096, start, 0.5)
+    for _, csv, stats in out:
+        assert csv == want
+        assert stats["ranged_rounds"] > 0 and stats["rounds"] > stats["ranged_rounds"]
 
 
 def test_stream_sync_finds_the_streams_word_starts():
