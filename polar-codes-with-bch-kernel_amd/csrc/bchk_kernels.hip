@@ -1637,50 +1637,49 @@ kaneko_search_kernel(SearchParams p) {
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
     AnWave *an = (AN && an_capable<M, TMAX>()) ? reinterpret_cast<AnWave *>(wbase + WB) : nullptr;
-    if constexpr (AN) {
-        if (p.in_queue) {  // concurrent with the first pass: take hand-offs as they come
-            uint32_t ndone = 0;
-            for (;;) {
-                uint32_t cw = 0, item = 0;
-                if (lane == 0) cw = tail_dequeue(p, item);
-                cw = (uint32_t)__shfl((int)cw, 0, 64);
-                item = (uint32_t)__shfl((int)item, 0, 64);
-                if (cw == kEmptySlot) break;
-                if (cw >= p.count) continue;  // never a valid slot value
-                search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item);
-                ++ndone;
-            }
-            wave_done(p, lane, ndone);
-            return;
-        }
-    }
-    if (!p.queue) {
-        const uint32_t stride = gridDim.x * kWavesPerBlock;
-        uint32_t ndone = 0;
-        for (uint32_t cw = blockIdx.x * kWavesPerBlock + wid; cw < p.count; cw += stride, ++ndone)
-            search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, cw);
-        wave_done(p, lane, ndone);
-        return;
-    }
-    // Work queue left by the fast path: sub-queue x holds items x, x+8, x+16, ...; a wave
-    // drains its own XCD's sub-queue first (one L2-local atomic per codeword), then steals.
-    const uint32_t total = *p.qcount;
-    const uint32_t nfront = p.qfront_n ? *p.qfront_n : total;  // items past it: the back
-    if ((blockIdx.x * kWavesPerBlock + wid) >= total) return;  // more waves than work
-    int x = xcc_id();
+    // Three sources of codewords -- the first pass's hand-offs as they come (the analytic
+    // tail beside the first pass), grid-stride over the batch (no queue), or the work queue
+    // left by the fast path (sub-queue x holds items x, x+8, ...; a wave drains its own
+    // XCD's sub-queue first, one L2-local atomic per codeword, then steals) -- feeding ONE
+    // call of search_codeword: with a single call site it is inlined, so the LDS state and
+    // the parameters stay in their own address spaces (ds_* and scalar loads). A second call
+    // site made it an outlined function taking generic pointers: every LDS access a flat
+    // access and the parameter block spilled to scratch.
+    const bool live = AN && p.in_queue;
+    const uint32_t stride = gridDim.x * kWavesPerBlock;
+    uint32_t gs = blockIdx.x * kWavesPerBlock + wid;
+    const uint32_t total = (!live && p.queue) ? *p.qcount : 0u;
+    const uint32_t nfront = (!live && p.queue && p.qfront_n) ? *p.qfront_n : total;  // past it: the back
+    if (!live && p.queue && gs >= total) return;  // more waves than work
+    int x = xcc_id(), exhausted = 0;
     uint32_t ndone = 0;
-    for (int exhausted = 0; exhausted < 8;) {
-        uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(p.heads + 32 * x, 1u);
-        k = (uint32_t)__shfl((int)k, 0, 64);
-        const uint32_t item = (uint32_t)x + 8u * k;
-        if (item >= total) {
-            x = (x + 1) & 7;
-            ++exhausted;
-            continue;
+    for (;;) {
+        uint32_t cw = kEmptySlot, item = 0;
+        if (live) {
+            if (lane == 0) cw = tail_dequeue(p, item);
+            cw = (uint32_t)__shfl((int)cw, 0, 64);
+            item = (uint32_t)__shfl((int)item, 0, 64);
+            if (cw == kEmptySlot) break;
+            if (cw >= p.count) continue;  // never a valid slot value
+        } else if (!p.queue) {
+            if (gs >= p.count) break;
+            cw = gs;
+            item = gs;
+            gs += stride;
+        } else {
+            if (exhausted >= 8) break;
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(p.heads + 32 * x, 1u);
+            k = (uint32_t)__shfl((int)k, 0, 64);
+            item = (uint32_t)x + 8u * k;
+            if (item >= total) {
+                x = (x + 1) & 7;
+                ++exhausted;
+                continue;
+            }
+            const uint32_t qi = item < nfront ? item : p.count - 1u - (item - nfront);
+            cw = p.queue[qi];
         }
-        const uint32_t qi = item < nfront ? item : p.count - 1u - (item - nfront);
-        const uint32_t cw = p.queue[qi];
         if (cw < p.count)  // never otherwise: no access outside the batch
             search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item);
         ++ndone;
@@ -2256,8 +2255,10 @@ static hipError_t launch_first_impl(const SearchParams &p, size_t lds, hipStream
 bool select_first_long(int m, int t, FastFn *out) {
 #define BCHK_FIRST(MM, TT) \
     if (m == MM && t <= TT) { *out = &launch_first_impl<MM, TT>; return true; }
+#ifndef BCHK_ISA_ONLY
     BCHK_FIRST(7, 8) BCHK_FIRST(7, 16) BCHK_FIRST(7, 32)
     BCHK_FIRST(8, 15) BCHK_FIRST(8, 16) BCHK_FIRST(8, 32)
+#endif
 #undef BCHK_FIRST
     return false;
 }
@@ -2298,6 +2299,9 @@ static KernelSet make_set() {
 bool select_kernels(int m, int t, KernelSet *out) {
 #define BCHK_TRY(MM, TT) \
     if (m == MM && t <= TT) { *out = make_set<MM, TT>(); return true; }
+#ifdef BCHK_ISA_ONLY  // ISA inspection builds: the headline code's kernels only
+    BCHK_TRY(6, 6)
+#else
     BCHK_TRY(2, 1)
     BCHK_TRY(3, 3)
     BCHK_TRY(4, 2) BCHK_TRY(4, 7)
@@ -2305,6 +2309,7 @@ bool select_kernels(int m, int t, KernelSet *out) {
     BCHK_TRY(6, 6) BCHK_TRY(6, 12) BCHK_TRY(6, 31)
     BCHK_TRY(7, 8) BCHK_TRY(7, 16) BCHK_TRY(7, 32)
     BCHK_TRY(8, 15) BCHK_TRY(8, 16) BCHK_TRY(8, 32)
+#endif
 #undef BCHK_TRY
     return false;
 }

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 from bchk_pkg import load  # noqa: E402
 
 F = load()
-cfgs = [(15, 5.0, 4), (15, 5.0, 2), (15, 4.0, 4), (-1, 5.0, 4)]
+cfgs = [(15, 5.0, 8), (15, 4.0, 8), (-1, 5.0, 8), (15, 5.0, 4)]
 if len(sys.argv) > 1:
     cfgs = cfgs[:int(sys.argv[1])]
 for J, snr, limit in cfgs:
