@@ -205,9 +205,9 @@ SyndKeyFn synd_key_fn(int m) {
 
 struct HostTable {
     int m = 0, t = 0;
-    uint32_t bbits = 0, max_probe = 0;
+    uint32_t bbits = 0, max_probe = 0, kbits = 0, tbits = 0;
     size_t keys = 0;
-    std::vector<uint64_t> slots;  // [nbuckets][kTabSlots][2]
+    std::vector<uint64_t> slots;  // [nbuckets][kTabSlots]
 };
 
 // Packed position fields (m bits each, ascending, unused fields all ones) of the pattern
@@ -226,24 +226,28 @@ uint64_t pack_leader(uint64_t e, int s, int kf, int m, int n, int t) {
 }
 
 // Insert (key, positions) unless the key is present (then they must agree: the coset
-// leader is unique). Returns false on a disagreement (a logic error).
-bool tab_insert(HostTable &h, uint64_t key, uint64_t mask) {
+// leader is unique). Returns 0, 1 on a disagreement (a logic error), 2 when the key would
+// sit 2^kTabDistBits buckets or more past its home (the caller grows the table).
+int tab_insert(HostTable &h, uint64_t key, uint64_t fields) {
+    const SyndTable T{nullptr, h.bbits, 0, h.kbits, h.tbits};
+    const TabHome H = tab_home(key, T);
+    const uint64_t tm = (1ull << h.tbits) - 1ull;
     const uint32_t bm = (1u << h.bbits) - 1u;
-    uint32_t b = tab_hash(key, h.bbits);
-    for (uint32_t p = 0;; ++p) {
-        uint64_t *bk = h.slots.data() + (size_t)b * (2 * kTabSlots);
+    uint32_t b = H.b;
+    for (uint32_t p = 0; p < (1u << kTabDistBits); ++p, b = (b + 1u) & bm) {
+        const uint64_t tag = H.tag | p;
+        uint64_t *bk = h.slots.data() + (size_t)b * kTabSlots;
         for (int j = 0; j < kTabSlots; ++j) {
-            if (bk[2 * j] == key) return bk[2 * j + 1] == mask;
-            if (bk[2 * j] == 0) {
-                bk[2 * j] = key;
-                bk[2 * j + 1] = mask;
+            if ((bk[j] & tm) == tag) return (bk[j] >> h.tbits) == fields ? 0 : 1;
+            if (bk[j] == 0) {
+                bk[j] = (fields << h.tbits) | tag;
                 h.max_probe = std::max(h.max_probe, p + 1);
                 ++h.keys;
-                return true;
+                return 0;
             }
         }
-        b = (b + 1u) & bm;
     }
+    return 2;
 }
 
 int build_table(const Field &f, int t, HostTable &h) {
@@ -261,16 +265,21 @@ int build_table(const Field &f, int t, HostTable &h) {
     // raw-region keys: every coprime syndrome zero (the key's region is the last one)
     int K = 0;
     for (int q = 0; q < t; ++q) K += f_coprime(q, n) ? 1 : 0;
-    // table size: <= ~50 % of slots used (orbits ~ C(n, <=t) / (n m), plus raw keys)
+    // table size: at most half of the slots used (orbits ~ C(n, <=t) / (n m), plus raw
+    // keys); BCHK_TAB_MAXLOAD (experiments) sets another bound
     double est = 0.0, c = 1.0;
     for (int w = 1; w <= t; ++w) {
         c = c * (n - w + 1) / w;
         est += c;
     }
     est = est / ((double)n * m) * 1.05 + 64;
+    double maxload = 0.5;
+    if (const char *ml = getenv("BCHK_TAB_MAXLOAD")) maxload = std::min(0.95, std::max(0.05, atof(ml)));
     h.bbits = 1;
-    while ((double)(kTabSlots << h.bbits) * 0.5 < est) ++h.bbits;
-    h.slots.assign((size_t(kTabSlots) << h.bbits) * 2, 0);
+    while ((double)(kTabSlots << h.bbits) * maxload < est) ++h.bbits;
+    h.kbits = (uint32_t)tab_kbits(m, t);
+    h.bbits = std::min(h.bbits, h.kbits);  // tiny key spaces: one bucket per key
+    while (!tab_fits(m, t, (int)h.bbits) && (int)h.bbits < (int)h.kbits) ++h.bbits;  // a 32-bit tag
     // enumerate in parallel (threads own second positions), insert serially
     const int hw = (int)std::thread::hardware_concurrency();
     const int nth = std::max(1, std::min(16, hw > 0 ? hw : 1));
@@ -278,7 +287,7 @@ int build_table(const Field &f, int t, HostTable &h) {
     auto emit = [&](std::vector<uint64_t> &out, uint64_t S, uint64_t pat) {
         const uint32_t Sw[2] = {(uint32_t)S, (uint32_t)(S >> 32)};
         const SyndKey k = keyf(Sw, t, lg);
-        if (((k.key - 1) >> 32) < (uint64_t)K) {  // a normalised region
+        if ((k.key >> tab_vbits(m, t)) < (uint64_t)K) {  // a normalised region
             out.push_back(k.key);
             out.push_back(pack_leader(pat, k.s, k.kf, m, n, t));
             return;
@@ -320,12 +329,24 @@ int build_table(const Field &f, int t, HostTable &h) {
             }
         });
     for (auto &x : th) x.join();
-    for (auto &v : found) {
-        for (size_t i = 0; i < v.size(); i += 2)
-            if (!tab_insert(h, v[i], v[i + 1]))
-                return fail(BCHK_EINVAL, "syndrome table: two leaders for one key (m=%d t=%d)", m, t);
-        std::vector<uint64_t>().swap(v);
+    // insert; a key too far from its home grows the table (a larger bbits also leaves fewer
+    // quotient bits, so the slot always fits: syndtab_feasible checked bbits = 1)
+    for (;; ++h.bbits) {
+        if (h.bbits > h.kbits || !tab_fits(m, t, (int)h.bbits))
+            return fail(BCHK_EINVAL, "syndrome table: no layout (m=%d t=%d)", m, t);
+        h.tbits = (uint32_t)tab_tbits(m, t, (int)h.bbits);
+        h.slots.assign(size_t(kTabSlots) << h.bbits, 0);
+        h.keys = 0;
+        h.max_probe = 0;
+        int rc = 0;
+        for (auto &v : found) {
+            for (size_t i = 0; i < v.size() && !rc; i += 2) rc = tab_insert(h, v[i], v[i + 1]);
+            if (rc) break;
+        }
+        if (rc == 1) return fail(BCHK_EINVAL, "syndrome table: two leaders for one key (m=%d t=%d)", m, t);
+        if (rc == 0) break;
     }
+    for (auto &v : found) std::vector<uint64_t>().swap(v);
     return 0;
 }
 
@@ -520,6 +541,8 @@ int ensure_table(bchk_ctx *c) {
     c->tab.slots = d;
     c->tab.bbits = h->bbits;
     c->tab.max_probe = h->max_probe;
+    c->tab.kbits = h->kbits;
+    c->tab.tbits = h->tbits;
     return 0;
 }
 
@@ -1482,7 +1505,7 @@ int bchk_syndrome_table_query(int m, int t, const uint32_t *synd, size_t N, uint
     TableDesc td{};
     const std::vector<uint8_t> blob = make_tables(f, t, &td);
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(blob.data() + td.off_log);
-    SyndTable T{h->slots.data(), h->bbits, h->max_probe};
+    SyndTable T{h->slots.data(), h->bbits, h->max_probe, h->kbits, h->tbits};
     for (size_t i = 0; i < N; ++i) {
         uint32_t Sw[2] = {0, 0};
         for (int q = 0; q < t; ++q) Sw[q >> 2] |= (synd[i * t + q] & 0xFFu) << (8 * (q & 3));

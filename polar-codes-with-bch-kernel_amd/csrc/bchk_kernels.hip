@@ -319,17 +319,17 @@ __device__ __forceinline__ void decode_chunks(const Prep<M, TMAX> &P, uint64_t b
     if constexpr (TAB) {
         // the decoder as a table lookup (bchk_syndtab.h): identical result
         SyndKey K[G];
-        uint32_t hb[G];
+        TabHome H[G];
         TabBucket B[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             K[g] = synd_key<M, TMAX>(Sw[g], t, lg);
-            hb[g] = tab_hash(K[g].key, T.bbits);
+            H[g] = tab_home(K[g].key, T);
         }
 #pragma unroll
-        for (int g = 0; g < G; ++g) tab_load(T, hb[g], B[g]);
+        for (int g = 0; g < G; ++g) tab_load(T, H[g].b, B[g]);
 #pragma unroll
-        for (int g = 0; g < G; ++g) ok[g] = tab_finish<M, TMAX>(T, K[g], hb[g], B[g], E[g].w[0]);
+        for (int g = 0; g < G; ++g) ok[g] = tab_finish<M, TMAX>(T, K[g], H[g], B[g], E[g].w[0]);
     } else {
 #pragma unroll
         for (int g = 0; g < G; ++g) ok[g] = alg_decode_word<M, TMAX>(ex, lg, chien, Sw[g], t, E[g]);
@@ -1613,10 +1613,13 @@ __device__ uint32_t tail_dequeue(const SearchParams &p, uint32_t &item) {
     return kEmptySlot;
 }
 
-#ifdef BCHK_SEARCH_WPE  // experiment builds (make wpe): waves per SIMD the registers must allow
+// Waves per SIMD the registers must allow: 5 for the first pass with the syndrome table
+// (its LDS allows 5 workgroups per CU; left alone it takes 98 VGPRs, 4 waves), the compiler's
+// choice otherwise (the tail instance needs ~220). BCHK_SEARCH_WPE: experiment builds.
+#ifdef BCHK_SEARCH_WPE
 #define BCHK_SEARCH_ATTR __attribute__((amdgpu_waves_per_eu(BCHK_SEARCH_WPE)))
 #else
-#define BCHK_SEARCH_ATTR
+#define BCHK_SEARCH_ATTR __attribute__((amdgpu_waves_per_eu((TAB && !AN) ? 5 : 1)))
 #endif
 template <int M, int TMAX, bool TAB, bool AN>
 __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) BCHK_SEARCH_ATTR

@@ -15,14 +15,19 @@
 // S_j is nonzero, the shift s with alpha^(j s) S_j = 1 is applied to all syndromes; S_j
 // (= 1) and the zero syndromes before it leave the key. The key is (region k = ordinal of
 // q*, packed remaining syndromes); syndromes whose coprime entries are all zero form the
-// last region, keyed by the raw remaining syndromes (s = 0). The table stores, per key,
-// positions of the normalised pattern; the caller maps them back. For BCH(63,30,13) that is
-// ~1.2 M shift orbits of the 75.6 M patterns, held in
-// an open-addressed table of 64-B buckets (4 slots of {key, positions}). Squaring all
-// syndromes (the Frobenius map: positions times 2 mod n) also preserves correctability,
-// so keys are canonical over that orbit too: ~0.2 M keys, 8 MiB, one bucket load per
-// lookup in the common case, mostly L2 / Infinity-Cache resident while the search kernels
-// run. Built once per (m, t) on the host, uploaded once per device.
+// last region, keyed by the raw remaining syndromes (s = 0). Squaring all syndromes (the
+// Frobenius map: positions times 2 mod n) also preserves correctability, so keys are
+// canonical over that orbit too: ~0.2 M keys for BCH(63,30,13) (of 75.6 M patterns).
+//
+// Slots are 8 B, as a quotient table: the key (region, canonical fields) is mixed by an
+// invertible multiplication mod 2^kbits; the top bbits of the product pick the home bucket
+// and only the rest (the quotient) is stored, with the slot's distance from home (linear
+// probing over 64-B buckets of 8 slots, at most 8 buckets) and all t position fields. The
+// low 32 bits hold the tag (occupied bit | quotient | distance), so a slot test is one
+// 32-bit compare; the fields sit above it (BCH(63,30,13): 20-bit tag + 36 field bits). At load
+// <= 1/2 the table is 4 MiB at BCH(63,30,13) (the 16-B {key, positions} slots of rounds 1-2
+// made it 8 MiB), one 64-B request per lookup in the common case. Built once per (m, t) on
+// the host, uploaded once per device.
 //
 // tests/test_syndtab.py checks every lookup against the oracle's Decoder::decode (the small
 // codes exhaustively); tests/test_gpu_parity.py runs every path with and without it.
@@ -37,14 +42,16 @@
 
 namespace bchk {
 
-constexpr int kTabMaxBits = 30;  // m * (t - 1) <= 30: region index fits 30 bits
-constexpr int kTabSlots = 4;     // slots per 64-B bucket
+constexpr int kTabMaxBits = 30;  // m * (t - 1) <= 30
+constexpr int kTabSlots = 8;     // 8-B slots per 64-B bucket
 
-// Device view: buckets of kTabSlots slots {key (0 = empty), error mask}.
+// Device view: buckets of kTabSlots slots (layout above; 0 = empty).
 struct SyndTable {
-    const uint64_t *slots;  // [nbuckets][kTabSlots][2], null = no table (BM + Chien)
+    const uint64_t *slots;  // [nbuckets][kTabSlots], null = no table (BM + Chien)
     uint32_t bbits;         // log2(nbuckets)
     uint32_t max_probe;     // longest probe sequence of any key, in buckets (from the build)
+    uint32_t kbits;         // bits of a canonical key (tab_kbits)
+    uint32_t tbits;         // bits of a slot's tag (tab_tbits)
 };
 
 __host__ __device__ constexpr int f_gcd(int a, int b) { return b ? f_gcd(b, a % b) : a; }
@@ -55,8 +62,29 @@ __host__ __device__ constexpr int f_inv(int j, int n) {  // j^-1 mod n (gcd(j, n
 }
 __host__ __device__ constexpr bool f_coprime(int q, int n) { return f_gcd(2 * q + 1, n) == 1; }
 
-inline bool syndtab_feasible(int m, int t) {
-    return m <= 6 && t >= 1 && m * (t - 1) <= kTabMaxBits;  // masks are one u64 (n <= 63)
+constexpr int kTabDistBits = 3;  // slot distance from its home bucket: < 8 buckets
+constexpr uint64_t kTabMult = 0x9E3779B97F4A7C15ull;  // odd: invertible mod 2^kbits
+
+// bits of the canonical key: region above m (t - 1) field bits (synd_key)
+__host__ __device__ __forceinline__ int tab_vbits(int m, int t) { return m * (t - 1); }
+inline int tab_kbits(int m, int t) {
+    const int n = (1 << m) - 1;
+    int K = 0;  // coprime odd indices: the last region's ordinal
+    for (int q = 0; q < t; ++q) K += f_coprime(q, n) ? 1 : 0;
+    int rb = 0;
+    while ((1 << rb) < K + 1) ++rb;
+    return tab_vbits(m, t) + rb;
+}
+// a slot: t fields of m bits | tag = occupied bit | quotient (kbits - bbits) | distance (3)
+inline int tab_tbits(int m, int t, int bbits) { return 1 + (tab_kbits(m, t) - bbits) + kTabDistBits; }
+inline bool tab_fits(int m, int t, int bbits) {
+    return tab_tbits(m, t, bbits) <= 32 && tab_tbits(m, t, bbits) + m * t <= 64;
+}
+constexpr int kTabMaxBucketBits = 20;  // 64 MiB
+inline bool syndtab_feasible(int m, int t) {  // n <= 63: one u64 mask; a layout within 64 MiB
+    if (m > 6 || t < 1 || m * (t - 1) > kTabMaxBits) return false;
+    const int kb = tab_kbits(m, t);
+    return tab_fits(m, t, kb < kTabMaxBucketBits ? kb : kTabMaxBucketBits);
 }
 
 // Per-(n, TMAX) constants, evaluated at compile time: coprimality of j = 2q + 1 and its
@@ -74,7 +102,7 @@ struct TabConsts {
 };
 
 struct SyndKey {
-    uint64_t key;  // (region << 32 | canonical packed log-syndromes) + 1, never 0
+    uint64_t key;  // region << m (t - 1) | canonical packed log-syndromes
     int s;         // normalising shift
     int kf;        // Frobenius power of the canonical form
     int t;         // position fields in a table entry
@@ -149,19 +177,30 @@ __host__ __device__ __forceinline__ SyndKey synd_key(const uint32_t *Sw, int t,
         best = cur < best ? cur : best;
     }
     SyndKey out;
-    out.key = (((uint64_t)k << 32) | best) + 1ull;
+    out.key = ((uint64_t)k << tab_vbits(M, t)) | best;
     out.s = s;
     out.kf = kf;
     out.t = t;
     return out;
 }
 
-__host__ __device__ __forceinline__ uint32_t tab_hash(uint64_t key, uint32_t bbits) {
-    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - bbits));
+// Home bucket and quotient of a key: h = key * kTabMult mod 2^kbits (a bijection), home =
+// its top bbits, quotient = the rest.
+struct TabHome {
+    uint32_t b;     // home bucket
+    uint32_t tag;   // the slot's tag at distance 0: 1 | quotient | 0
+};
+__host__ __device__ __forceinline__ TabHome tab_home(uint64_t key, const SyndTable &T) {
+    const uint64_t h = (key * kTabMult) & ((1ull << T.kbits) - 1ull);
+    const int qb = (int)T.kbits - (int)T.bbits;
+    TabHome r;
+    r.b = (uint32_t)(h >> qb);
+    r.tag = (1u << (T.tbits - 1u)) | ((uint32_t)(h & ((1ull << qb) - 1ull)) << kTabDistBits);
+    return r;
 }
 
 // Stored pattern: t position fields of m bits (unused fields all ones) of the canonical
-// syndrome's leader P = 2^kf (e + s). Back to e: p = 2^-kf p' - s (mod n) per field.
+// syndrome's leader P = 2^kf (e + s), ascending. Back to e: p = 2^-kf p' - s (mod n).
 template <int M, int TMAX>
 __host__ __device__ __forceinline__ uint64_t tab_unmap(uint64_t packed, int s, int kf, int t) {
     constexpr int N = (1 << M) - 1;
@@ -176,50 +215,55 @@ __host__ __device__ __forceinline__ uint64_t tab_unmap(uint64_t packed, int s, i
     return E;
 }
 
-// One 64-B bucket: kTabSlots {key, packed positions}.
+// One 64-B bucket: kTabSlots slots.
 struct TabBucket {
-    uint64_t k[kTabSlots], v[kTabSlots];
+    uint64_t k[kTabSlots];
 };
 
 __host__ __device__ __forceinline__ void tab_load(const SyndTable &T, uint32_t b, TabBucket &B) {
-    const uint64_t *bk = T.slots + (size_t)b * (2 * kTabSlots);
+    const uint64_t *bk = T.slots + (size_t)b * kTabSlots;
 #pragma unroll
-    for (int j = 0; j < kTabSlots; ++j) {
-        B.k[j] = bk[2 * j];
-        B.v[j] = bk[2 * j + 1];
-    }
+    for (int j = 0; j < kTabSlots; ++j) B.k[j] = bk[j];
 }
 
-// Finish a lookup from its home bucket (already loaded): further buckets only when the
-// home bucket is full without the key (linear probing; no key sits more than
-// T.max_probe - 1 buckets past its home).
+// Finish a lookup from its home bucket (already loaded): a slot matches when its bits above
+// the fields are the key's tag at the bucket's distance from home; further buckets only
+// when the home bucket is full without the key (no key sits more than T.max_probe - 1
+// buckets past its home).
 template <int M, int TMAX>
-__host__ __device__ __forceinline__ bool tab_finish(const SyndTable &T, const SyndKey &K,
-                                                    uint32_t b, const TabBucket &B0, uint64_t &E) {
+__host__ __device__ __forceinline__ bool tab_finish(const SyndTable &T, const SyndKey &K, const TabHome &H,
+                                                    const TabBucket &B0, uint64_t &E) {
+    const uint32_t tm = (1u << T.tbits) - 1u;
     uint64_t v = 0;
     bool hit = false, open = false;
 #pragma unroll
     for (int j = 0; j < kTabSlots; ++j) {
-        v = (B0.k[j] == K.key) ? B0.v[j] : v;
-        hit = hit || B0.k[j] == K.key;
-        open = open || B0.k[j] == 0ull;
+        const uint32_t lo = (uint32_t)B0.k[j];
+        const bool h = (lo & tm) == H.tag;
+        v = h ? B0.k[j] : v;
+        hit = hit || h;
+        open = open || lo == 0u;
     }
     if (!hit && !open) {
         const uint32_t bm = (1u << T.bbits) - 1u;
+        uint32_t b = H.b;
         for (uint32_t p = 1; p < T.max_probe; ++p) {
             b = (b + 1u) & bm;
+            const uint32_t tag = H.tag | p;
             TabBucket B;
             tab_load(T, b, B);
 #pragma unroll
             for (int j = 0; j < kTabSlots; ++j) {
-                v = (B.k[j] == K.key) ? B.v[j] : v;
-                hit = hit || B.k[j] == K.key;
-                open = open || B.k[j] == 0ull;
+                const uint32_t lo = (uint32_t)B.k[j];
+                const bool h = (lo & tm) == tag;
+                v = h ? B.k[j] : v;
+                hit = hit || h;
+                open = open || lo == 0u;
             }
             if (hit || open) break;
         }
     }
-    E = hit ? tab_unmap<M, TMAX>(v, K.s, K.kf, K.t) : 0ull;
+    E = hit ? tab_unmap<M, TMAX>(v >> T.tbits, K.s, K.kf, K.t) : 0ull;
     return hit;
 }
 
@@ -229,10 +273,10 @@ template <int M, int TMAX>
 __host__ __device__ __forceinline__ bool tab_decode(const SyndTable &T, const uint32_t *Sw, int t,
                                                     const uint16_t *lg, uint64_t &E) {
     const SyndKey K = synd_key<M, TMAX>(Sw, t, lg);
-    const uint32_t b = tab_hash(K.key, T.bbits);
+    const TabHome H = tab_home(K.key, T);
     TabBucket B;
-    tab_load(T, b, B);
-    return tab_finish<M, TMAX>(T, K, b, B, E);
+    tab_load(T, H.b, B);
+    return tab_finish<M, TMAX>(T, K, H, B, E);
 }
 
 }  // namespace bchk

@@ -87,7 +87,8 @@ def test_table_size_and_probes():
     # one key per (cyclic shift x Frobenius) orbit of the 75.6 M weight <= 6 patterns of
     # length 63: ~75.6 M / (63 * 6), plus orbits smaller than 378 and raw-region keys
     assert 195_000 < keys < 215_000
-    assert nbytes <= 16 << 20 and 1 <= probe <= 16
+    # 8-B slots in 64-B buckets at load <= 1/2: 4 MiB, the size of one XCD's L2
+    assert nbytes <= 4 << 20 and 1 <= probe <= 16
 
 
 def test_table_rejects_infeasible():
