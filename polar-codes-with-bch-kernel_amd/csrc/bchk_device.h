@@ -132,6 +132,10 @@ struct SearchParams {
     // cnt_reduce_kernel folds into the caller's totals
     const uint8_t *tx;
     unsigned long long *cnt;
+    // fast kernel (bchk_fast.hip), experiment: blocks of the first round and the start
+    // delay of its second half in cycles (0: none)
+    uint32_t fast_blocks;
+    uint32_t fast_stagger;
 };
 constexpr int kCntSlots = 512;
 constexpr int kCntStride = 16;  // u64 per slot: one 128-B line

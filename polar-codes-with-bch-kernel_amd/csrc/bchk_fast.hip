@@ -117,6 +117,12 @@ kaneko_fast_kernel(SearchParams p) {
     double *stage = reinterpret_cast<double *>(smem + ((p.td.bytes + 15) & ~15u) + wid * kStageBytes);
     const uint32_t cw0 = (blockIdx.x * kFastWaves + wid) * 64u;
     if (cw0 >= p.count) return;
+    // experiment (BCHK_FAST_STAGGER): the first round's second block on each CU starts
+    // p.fast_stagger cycles late, so the CU's two blocks load and compute out of phase
+    if (p.fast_stagger && blockIdx.x >= p.fast_blocks / 2 && blockIdx.x < p.fast_blocks) {
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < p.fast_stagger) __builtin_amdgcn_s_sleep(8);
+    }
     const uint32_t cw = cw0 + (uint32_t)lane;
     const bool live = cw < p.count;
     const int t = p.t;

@@ -426,6 +426,9 @@ struct bchk_ctx {
     // BCHK_TAIL_INLINE=1: the first pass IS the analytic-tail kernel instance -- a codeword
     // past the chunk limit is finished by the same wave at once, no second kernel
     bool tail_inline = false;
+    // lane fast kernel, experiment: the first round's second block per CU starts
+    // BCHK_FAST_STAGGER cycles late (fast_blocks = the first round's blocks)
+    uint32_t fast_blocks = 0, fast_stagger = 0;
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
     // hybrid tail: a first-pass hand-off whose loop bound is below this goes to a cooperative
@@ -634,6 +637,10 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
         if (c->heavy_first && c->m <= 6) {  // the lane fast kernel (m >= 7: the first kernel)
             f.qfront = ctrl + kQFront;
             f.qback = ctrl + kQBack;
+        }
+        if (c->m <= 6) {
+            f.fast_blocks = c->fast_blocks;
+            f.fast_stagger = c->fast_stagger;
         }
         HIP_TRY(c->fast(f, c->lds_fast, s));
     }
@@ -855,6 +862,10 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (getenv("BCHK_TAIL_DIAG")) c->tail_diag_on = true;
     if (const char *tc = getenv("BCHK_TAIL_CONCURRENT")) c->tail_concurrent = atoi(tc) != 0;
     if (const char *ti = getenv("BCHK_TAIL_INLINE")) c->tail_inline = atoi(ti) != 0;
+    if (const char *fs = getenv("BCHK_FAST_STAGGER")) {
+        c->fast_stagger = (uint32_t)std::max(0, atoi(fs));
+        c->fast_blocks = 2u * (uint32_t)prop.multiProcessorCount;  // the first round's blocks
+    }
     if (const char *tb = getenv("BCHK_TAIL_BLOCKS")) c->tail_conc_blocks = std::max(1, atoi(tb));
     if (const char *tm = getenv("BCHK_TAIL_MIN_BOUND")) c->tail_min_bound = strtoull(tm, nullptr, 10);
     if (const char *hf = getenv("BCHK_HEAVY_FIRST")) c->heavy_first = atoi(hf) != 0;
