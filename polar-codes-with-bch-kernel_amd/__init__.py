@@ -34,7 +34,7 @@ EXPORTS = (
     "bchk_generate_host", "bchk_generate_host_draws", "bchk_generate_device", "bchk_sweep_device", "bchk_rng_jump", "bchk_sweep_block", "bchk_sweep_range", "bchk_stream_skip",
     "bchk_stream_sync", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
     "bchk_profile_read", "bchk_profile_read_stages", "bchk_path_counts", "bchk_tail_count",
-    "bchk_tail_stats", "bchk_tail_diag_read", "bchk_set_fast_path", "bchk_set_analytic",
+    "bchk_tail_stats", "bchk_tail_diag_read", "bchk_tail_prof_read", "bchk_set_fast_path", "bchk_set_analytic",
     "bchk_set_chunk_limit", "bchk_set_syndrome_table",
     "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_polar_create", "bchk_polar_create_kdir",
     "bchk_polar_destroy", "bchk_polar_params", "bchk_polar_decode_host", "bchk_polar_decode_device",
@@ -127,6 +127,7 @@ def lib():
     L.bchk_tail_count.argtypes = [vp, C.POINTER(u64)]
     L.bchk_tail_stats.argtypes = [vp, C.POINTER(u64)]
     L.bchk_tail_diag_read.argtypes = [vp, C.POINTER(u64), sz, C.POINTER(u64)]
+    L.bchk_tail_prof_read.argtypes = [vp, C.POINTER(u64), sz]
     L.bchk_profile_read_stages.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
     L.bchk_set_analytic.argtypes = [vp, i32]
     L.bchk_set_chunk_limit.argtypes = [vp, C.c_uint32]
@@ -337,6 +338,13 @@ class KanekoKernelProcessor:
         _check(lib().bchk_tail_diag_read(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), items,
                                          C.byref(n)))
         return out[:min(items, n.value)]
+
+    def tail_prof(self, items=65536):
+        """Experiment builds (BCHK_AN_PROF): enumeration cycles by step phase per tail record."""
+        import numpy as np
+        out = np.zeros((items, 8), np.uint64)
+        _check(lib().bchk_tail_prof_read(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), items))
+        return out
 
     def set_analytic(self, enable=True):
         """Analytic tail of heavy codewords (results identical either way)."""

@@ -99,6 +99,9 @@ struct SearchParams {
     // search kernel: after chunk_limit exact chunks, finish the codeword from its candidate
     // codewords (bchk_kernels.hip, analytic tail) instead of handing it off; 0 = hand off
     int32_t analytic;
+    // analytic tail kernel: waves of a block whose queue is exhausted help a sibling decode
+    // the exact chunks of a split codeword (bchk_kernels.hip, HelpCtl); 0 = off
+    int32_t an_help;
     // analytic tail outcomes (null = not counted): [0] handed on to the cooperative kernel,
     // [1] finished from the candidates, [2] split (exact chunks, then the candidates),
     // [3] exact chunks of the splits

@@ -426,6 +426,9 @@ struct bchk_ctx {
     // BCHK_TAIL_INLINE=1: the first pass IS the analytic-tail kernel instance -- a codeword
     // past the chunk limit is finished by the same wave at once, no second kernel
     bool tail_inline = false;
+    // idle waves of the tail kernel help a sibling's split codeword decode its exact chunks
+    // (BCHK_AN_HELP=0: off; results identical either way)
+    bool an_help = true;
     // lane fast kernel, experiment: the first round's second block per CU starts
     // BCHK_FAST_STAGGER cycles late (fast_blocks = the first round's blocks)
     uint32_t fast_blocks = 0, fast_stagger = 0;
@@ -695,6 +698,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
         q.analytic = 1;
         q.tail_stats = ctrl + kTailStats;
         q.tail_rec = (TailRec *)P.l1rec.p;
+        q.an_help = (c->an_help && !tconc) ? 1 : 0;
         if (tconc) {  // take the first pass's hand-offs as they come, with their state
             q.in_queue = (uint32_t *)P.l1q.p;
             q.in_tail = ctrl + kL1Tail;
@@ -707,7 +711,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             HIP_TRY(hipMemsetAsync(c->tdiag.p, 0, c->tdiag.cap, s));
             q.tail_diag = (unsigned long long *)c->tdiag.p;
             q.tail_diag_count = ctrl + kTailStats + 16;
-            q.tail_diag_cap = (uint32_t)(c->tdiag.cap / 64);
+            q.tail_diag_cap = (uint32_t)(c->tdiag.cap / 128);  // second half: bchk_tail_prof_read
         }
         int tgrid = tabk ? c->grid_tail_tab : c->grid_tail;
         if (tconc || hybrid) tgrid = std::min(tgrid, c->tail_conc_blocks);  // CUs for the others
@@ -850,7 +854,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     }
     const size_t tb = (c->td.bytes + 15) & ~size_t(15);
     c->lds = tb + kWavesPerBlock * c->ks.wave_bytes;
-    c->lds_tail = tb + kWavesPerBlock * c->ks.tail_wave_bytes;
+    c->lds_tail = tb + kWavesPerBlock * c->ks.tail_wave_bytes + c->ks.tail_block_bytes;
     c->lds_alg = tb;
     if (select_fast(m, t, &c->fast))  // m >= 7: kaneko_first_kernel, the search kernel's layout
         c->lds_fast = m >= 7 ? c->lds : tb + fast_block_waves() * fast_wave_bytes();
@@ -862,6 +866,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (getenv("BCHK_TAIL_DIAG")) c->tail_diag_on = true;
     if (const char *tc = getenv("BCHK_TAIL_CONCURRENT")) c->tail_concurrent = atoi(tc) != 0;
     if (const char *ti = getenv("BCHK_TAIL_INLINE")) c->tail_inline = atoi(ti) != 0;
+    if (const char *ah = getenv("BCHK_AN_HELP")) c->an_help = atoi(ah) != 0;
     if (const char *fs = getenv("BCHK_FAST_STAGGER")) {
         c->fast_stagger = (uint32_t)std::max(0, atoi(fs));
         c->fast_blocks = 2u * (uint32_t)prop.multiProcessorCount;  // the first round's blocks
@@ -1449,9 +1454,17 @@ int bchk_tail_diag_read(bchk_ctx *c, uint64_t *out, size_t items, uint64_t *coun
     uint32_t n = 0;
     if (c->pipes.empty() || !c->pipes[0].ctrl.p) return 0;
     HIP_TRY(hipMemcpy(&n, (uint32_t *)c->pipes[0].ctrl.p + kTailStats + 16, 4, hipMemcpyDeviceToHost));
-    const size_t m = std::min<size_t>({items, (size_t)n, c->tdiag.cap / 64});
+    const size_t m = std::min<size_t>({items, (size_t)n, c->tdiag.cap / 128});
     HIP_TRY(hipMemcpy(out, c->tdiag.p, m * 64, hipMemcpyDeviceToHost));
     *count = n;
+    return 0;
+}
+
+int bchk_tail_prof_read(bchk_ctx *c, uint64_t *out, size_t items) {
+    if (!c || !out) return fail(BCHK_EINVAL, "NULL argument");
+    if (!c->tdiag.p) return 0;
+    const size_t cap = c->tdiag.cap / 128, m = std::min(items, cap);
+    HIP_TRY(hipMemcpy(out, (const uint8_t *)c->tdiag.p + cap * 64, m * 64, hipMemcpyDeviceToHost));
     return 0;
 }
 

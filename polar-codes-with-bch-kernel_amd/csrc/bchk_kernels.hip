@@ -603,7 +603,7 @@ struct AnNode {  // enumeration node: D_U = sel (bits over U indices)
     uint64_t rem;       // residual syndrome (zero: a codeword)
     int64_t sum;        // sum of a over D_U, fixed point (a lower bound)
     uint32_t sel, comb; // U indices; pattern bits of D_R for this D_U
-    uint32_t next, pad; // the next child to generate
+    uint32_t next, cls; // the next child to generate; the residual's class (leaf runs)
 };
 struct AnCand {
     uint64_t D;  // yH ^ c (positions)
@@ -634,8 +634,13 @@ struct AnWave {
     // rem0, identified by their bits at the span's pivot positions (cbits of them): cmask[c]
     // = the U elements whose residual has class c
     uint32_t cmask[32];
+    uint8_t ucls[kAnMaxU];  // class of U element q's residual (classes are linear)
     uint8_t cpiv[5];
     int32_t cbits;
+#ifdef BCHK_AN_PROF
+    // experiment builds: cycles of the enumeration by step phase (scripts/an_diag.py)
+    uint64_t prof[8];
+#endif
 };
 template <int M, int TMAX>
 constexpr bool an_capable() { return Geo<M>::NW == 1 && TMAX <= 8; }
@@ -711,13 +716,29 @@ __device__ __forceinline__ void an_emit(AnWave *A, uint32_t sel, int64_t usum, u
 // Returns 0, or why the candidate list is partial: 1 node budget, 2 stack, 3 list full.
 template <int TMAX>
 __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t rem0, uint32_t comb0,
-                             int nkern, uint64_t ifrom, uint64_t BM, double l0, double lcap,
+                             uint32_t cls0, int nkern, uint64_t ifrom, uint64_t BM, double l0, double lcap,
                              const double *ap, uint32_t budget, int lane, uint32_t &iters) {
     const int jb = BM > 1ull ? 64 - __builtin_clzll(BM - 1ull) : 0;  // patterns < BM: bits < jb
+#ifdef BCHK_AN_PROF
+    // [0] pops, [1] loads + single child + its drain, [2] leaf runs, [3] stack pushes,
+    // [4] emission batches, [5] their cycles, [6] leaf-run rounds, [7] steps
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tq = __builtin_amdgcn_s_memtime();
+#define AN_PF(i)                                            \
+    {                                                       \
+        const uint64_t tn_ = __builtin_amdgcn_s_memtime(); \
+        pf[i] += tn_ - tq;                                  \
+        tq = tn_;                                           \
+    }
+    auto pf_flush = [&]() {
+        if (lane == 0)
+            for (int i = 0; i < 8; ++i) A->prof[i] += pf[i];
+    };
+#else
+#define AN_PF(i)
+    auto pf_flush = [&]() {};
+#endif
     const int cbits = A->cbits;
-    int cpiv[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) cpiv[i] = A->cpiv[i];
     if (lane == 0) A->ncand = 0u;
     wave_sync();
     if (lane == 0 && rem0 == 0ull) an_emit<TMAX>(A, 0u, 0, comb0, 0, t, nkern, ifrom, BM, jb, l0, lcap, ap);
@@ -727,7 +748,7 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
     nd.sel = 0;
     nd.comb = comb0;
     nd.next = 0;
-    nd.pad = 0;
+    nd.cls = cls0;
     bool have = lane == 0 && t >= 1;
     int sp = 0, np = 0;  // stack and pending-emission counts
     uint32_t steps = 0;
@@ -755,6 +776,7 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         }
         ++iters;
         wave_sync();  // the pops are read before this step's pushes reuse their slots
+        AN_PF(0)
         const int depth = __popc(nd.sel);
         const int next = (int)nd.next;
         const int q = next < NU ? next : NU;  // NU: the sentinel (never fits)
@@ -765,11 +787,9 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         const int64_t anext = A->afix[q + 1 <= NU ? q + 1 : NU];
         const uint64_t rq = A->ru[qr];
         const uint32_t cq = A->cu[qr];
-        uint32_t cl = 0;
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-            if (i < cbits) cl |= (uint32_t)((nd.rem >> cpiv[i]) & 1ull) << i;
-        const uint32_t cmk = A->cmask[cbits >= 0 ? cl : 0];
+        const uint32_t uq = A->ucls[qr];
+        // the node carries its residual's class: no dependent load for the class mask
+        const uint32_t cmk = A->cmask[cbits >= 0 ? nd.cls : 0];
         const int64_t X = limfix - nd.sum;
         const bool valid = have && next < NU && depth < t && aq <= X;
         const int64_t cs = nd.sum + aq;
@@ -782,6 +802,7 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         const uint64_t crem = nd.rem ^ rq;
         const uint32_t ccomb = nd.comb ^ cq;
         const uint32_t csel = nd.sel | (1u << qr);
+        const uint32_t ccls = nd.cls ^ uq;
         // codewords (zero residual) that can still reach a pattern below BM wait for the
         // next batch of emissions (a whole wave processes 64 together)
         auto push = [&](bool c, uint32_t sel, uint32_t comb, int64_t sum) {
@@ -797,48 +818,72 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         };
         auto drain = [&]() {
             while (np >= 64) {
+#ifdef BCHK_AN_PROF
+                const uint64_t te_ = __builtin_amdgcn_s_memtime();
+#endif
                 wave_sync();
                 const AnPend e = A->pend[np - 1 - lane];
                 an_emit<TMAX>(A, e.sel, e.usum, e.comb, __popc(e.sel), t, nkern, ifrom, BM, jb, l0, lcap, ap);
                 np -= 64;
                 wave_sync();
+#ifdef BCHK_AN_PROF
+                pf[4] += 1;
+                pf[5] += __builtin_amdgcn_s_memtime() - te_;
+#endif
             }
         };
         push(single && crem == 0ull && (nkern > 0 || __popc(ccomb >> jb) <= t - depth - 1), csel, ccomb, cs);
         drain();
+        AN_PF(1)
         // a leaf run from q on: of the remaining children only those whose residual
-        // matches can be codewords, ascending until one is over the bound; 4 at a time
+        // matches can be codewords, ascending until one is over the bound; kAnLeaf per
+        // round (one LDS round trip), the pushes (rare: most fail the pattern filter) only
+        // when some lane has one
         uint32_t mm = run ? (cmk & ~((1u << qr) - 1u)) : 0u;
         while (ballot(mm != 0u)) {
-            int mi[4];
+#ifdef BCHK_AN_PROF
+            pf[6] += 1;
+#endif
+            constexpr int kAnLeaf = 4;  // measured: 8 per round visits more slots for the same rounds
+            int mi[kAnLeaf];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < kAnLeaf; ++i) {
                 mi[i] = mm ? (int)__builtin_ctz(mm) : NU;
                 mm &= mm - 1u;
             }
-            int64_t av[4];
-            uint32_t cv[4];
+            int64_t av[kAnLeaf];
+            uint32_t cv[kAnLeaf];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < kAnLeaf; ++i) {
                 av[i] = A->afix[mi[i]];
                 cv[i] = A->cu[mi[i] < NU ? mi[i] : 0];
             }
             bool stop = false;
+            uint32_t pm = 0u;  // elements to push
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < kAnLeaf; ++i) {
                 stop = stop || !(av[i] <= X);  // the sentinel at NU never fits
                 const uint32_t pc = nd.comb ^ cv[i];
-                push(!stop && (nkern > 0 || __popc(pc >> jb) <= t - depth - 1), nd.sel | (1u << (mi[i] & 31)), pc,
-                     nd.sum + av[i]);
+                if (!stop && (nkern > 0 || __popc(pc >> jb) <= t - depth - 1)) pm |= 1u << i;
             }
             if (stop) mm = 0u;
-            drain();
+            if (ballot(pm != 0u)) {
+#pragma unroll
+                for (int i = 0; i < kAnLeaf; ++i) {
+                    push(((pm >> i) & 1u) != 0u, nd.sel | (1u << (mi[i] & 31)), nd.comb ^ cv[i], nd.sum + av[i]);
+                    if (i % 4 == 3) drain();  // the pending list holds < 64 + 5 x 64
+                }
+            }
         }
+        AN_PF(2)
         // the parent stays open iff its next child fits too
         const bool cont = expand && anext <= X;
         const uint64_t em = ballot(cont);
         const int cnt = __popcll(em);
-        if (sp + cnt > kAnStack) return 2;
+        if (sp + cnt > kAnStack) {
+            pf_flush();
+            return 2;
+        }
         if (cont) {
             AnNode c = nd;
             c.next = (uint32_t)(q + 1);
@@ -850,13 +895,23 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
             nd.sum = cs;
             nd.sel = csel;
             nd.comb = ccomb;
+            nd.cls = ccls;
         }
         nd.next = (uint32_t)(q + 1);
         const bool valid_next = single;  // a leaf run ends the node
         have = valid_next;
         wave_sync();
-        if (++steps > budget / 8) return 1;  // the DP bound keeps real enumerations far below
+#ifdef BCHK_AN_PROF
+        pf[7] += 1;
+#endif
+        AN_PF(3)
+        if (++steps > budget / 8) {  // the DP bound keeps real enumerations far below
+            pf_flush();
+            return 1;
+        }
     }
+    pf_flush();
+#undef AN_PF
     return A->ncand <= (uint32_t)kAnCand ? 0 : 3;
 }
 
@@ -983,7 +1038,7 @@ __device__ int an_osd(const SearchState<1> &S, const Prep<M, TMAX> &P, AnWave *A
         r.sel = 0;
         r.comb = 0;
         r.next = 0;
-        r.pad = 0;
+        r.cls = 0;
         A->stack[0] = r;
     }
     sp = nf > 0 ? 1 : 0;
@@ -1055,6 +1110,10 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     const int t = p.t, J = p.J;
     AnPlan plan{0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_0 = p.tail_diag ? __builtin_amdgcn_s_memtime() : 0;
+#ifdef BCHK_AN_PROF
+    if (lane < 8) A->prof[lane] = 0;
+    wave_sync();
+#endif
     // NB pattern bits: every pattern any future bound admits, and |U| <= 32
     int NB;
     if (N >= 63) NB = 31;
@@ -1125,6 +1184,7 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     }
     const uint64_t rem0 = rdl64(v, N);
     const uint32_t comb0 = rdl(comb, N);
+    uint32_t cls0 = 0;
     if (p.tail_diag) plan.t_elim = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
     if (lane >= NB && lane < N) {
         const int q = lane - NB;
@@ -1170,6 +1230,8 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
                 if (lane == 0) A->cmask[c] = (uint32_t)(bm >> NB);
             }
         }
+        if (lane >= NB && lane < N) A->ucls[lane - NB] = (uint8_t)cls;
+        cls0 = rdl(cls, N);  // rem0's class
         if (lane == 0) {
             A->cbits = cbits;
 #pragma unroll
@@ -1210,7 +1272,7 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     if (NU < 4 || t <= 3 ||
         rdlf(P.asv[0], NB) + rdlf(P.asv[0], NB + 1) + rdlf(P.asv[0], NB + 2) + rdlf(P.asv[0], NB + 3) > full) {
         if (p.tail_diag) plan.t_setup = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
-        const int er = an_enumerate<TMAX>(A, NU, t, an_fix_up(full), rem0, comb0, nkern, ifrom, BM, l0, l0, ap,
+        const int er = an_enumerate<TMAX>(A, NU, t, an_fix_up(full), rem0, comb0, cls0, nkern, ifrom, BM, l0, l0, ap,
                                           2 * kAnBudget, lane, iters);
         if (!er) {
             plan.mode = 1;
@@ -1268,7 +1330,7 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
         const int L = 63 - (int)__builtin_clzll(fit);
         const bool whole = L == 63 && hi >= full;
         const double lim = whole ? full : (double)(L + 1) * delta * (1.0 - 0x1p-30);
-        const int er = an_enumerate<TMAX>(A, NU, t, an_fix_up(whole ? full : lim), rem0, comb0, nkern, ifrom, BM,
+        const int er = an_enumerate<TMAX>(A, NU, t, an_fix_up(whole ? full : lim), rem0, comb0, cls0, nkern, ifrom, BM,
                                           l0, whole ? l0 : lim, ap, budget * 2, lane, iters);
         if (er) {
             plan.fails |= 1 << er;
@@ -1355,6 +1417,227 @@ __device__ __forceinline__ TailRec tail_rec_load(const TailRec *src) {
     return r;
 }
 
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t *a, uint32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint64_t lds_ld64(const uint64_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st64(uint64_t *a, uint64_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+constexpr uint32_t kSpinLimit = 1u << 24;  // ~1 s of polling: a guard against logic errors
+// A bounded wait ran out (a logic error: its codeword stays unfinished): tell the host.
+__device__ __forceinline__ void flag_fault(const SearchParams &p, uint32_t bit) {
+    if (p.fault) atomicOr(p.fault, bit);
+}
+
+// ----------------------------------------- helper waves of the analytic tail kernel
+// At 5 dB the tail kernel holds about one heavy codeword per wave, most of them finish
+// within ~1.3e5 cycles, and the kernel's time is its slowest codeword's critical path. A
+// split codeword (plan mode 2) then decodes up to kAnExactChunks exact chunks one after
+// another. Waves of the same block whose queue is exhausted help: the owner publishes its
+// decode state (the pattern-syndrome inputs of decode_chunks) and the chunk range; helpers
+// claim chunks in order with a CAS on `next` (generation << 16 | chunk) and leave each one's
+// per-lane results in a ring slot tagged generation << 16 | chunk + 1; the owner consumes
+// the chunks in order -- the acceptance stays the owner's, in pattern order -- and decodes
+// a chunk itself whenever nobody has claimed it, so it never waits on an absent helper.
+// Every result is decode_chunks' own for that chunk: the output is unchanged.
+constexpr int kHelpSlots = 4;
+constexpr uint32_t kHelpNone = 0xFFFFu;  // chunk field: no chunk claimable
+struct HelpSlot {
+    uint64_t diff[64];
+    double l[64];
+    uint8_t m[64];
+    uint64_t okm;
+    uint32_t tag, pad;
+};
+struct HelpCtl {
+    uint32_t idle;      // waves of the block past their last codeword
+    uint32_t owner;     // wave id + 1 of the job's owner, 0: no job
+    uint32_t gen;       // the current job's generation (low 16 bits in next and the tags)
+    uint32_t next;      // gen << 16 | next unclaimed chunk (kHelpNone: closed or being set up)
+    uint32_t consumed;  // chunks the owner has taken, in order
+    uint32_t nch;       // chunks in the job
+    uint64_t base;      // first test pattern of chunk 0
+    int32_t t, pad;
+    uint32_t S0[2];
+    uint32_t Lo[2][64], scol[2][64];
+    uint64_t Plo[64];
+    int32_t ordb[64];
+    HelpSlot slot[kHelpSlots];
+};
+template <int M, int TMAX>
+constexpr int help_bytes() { return an_capable<M, TMAX>() ? (int)((sizeof(HelpCtl) + 15) & ~size_t(15)) : 0; }
+
+__device__ __forceinline__ uint32_t help_gen_next(uint32_t g) { return (g + 1u) & 0xFFFFu ? (g + 1u) & 0xFFFFu : 1u; }
+
+// Owner: publish a job of nch chunks from pattern base, when some sibling is idle (then
+// true: the caller takes its chunks through help_take and ends with help_close).
+template <int M, int TMAX>
+__device__ bool help_open(HelpCtl *H, const Prep<M, TMAX> &P, uint64_t base, uint32_t nch, int t, int wid,
+                          int lane) {
+    constexpr int W = Prep<M, TMAX>::W;
+    static_assert(W <= 2 && Geo<M>::NW == 1, "helper jobs: n <= 63, t <= 8");
+    uint32_t got = 0;
+    if (lane == 0 && nch >= 2u && lds_ld(&H->idle) > 0u) got = atomicCAS(&H->owner, 0u, (uint32_t)wid + 1u) == 0u;
+    got = (uint32_t)__shfl((int)got, 0, 64);
+    if (!got) return false;
+    const uint32_t g = help_gen_next(H->gen);  // only the owner writes gen
+    if (lane == 0) {
+        H->gen = g;
+        lds_st(&H->next, (g << 16) | kHelpNone);  // generation first: readers re-check it
+    }
+    wave_sync();
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        H->Lo[w][lane] = P.Lo[w];
+        H->scol[w][lane] = P.scol[w];
+    }
+    H->Plo[lane] = P.Plo.w[0];
+    H->ordb[lane] = P.ordb;
+    if (lane == 0) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) H->S0[w] = P.S0[w];
+        H->base = base;
+        H->nch = nch;
+        H->t = t;
+        H->consumed = 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wave_sync();
+    if (lane == 0) lds_st(&H->next, g << 16);
+    return true;
+}
+
+// Owner: the results of chunk k (in order). true: read from a helper's slot; false: the
+// owner claimed it and decodes it itself.
+__device__ bool help_take(HelpCtl *H, uint32_t k, uint64_t &diff, double &l, int &m, bool &ok, int lane,
+                          const SearchParams &p) {
+    const uint32_t g = H->gen;
+    HelpSlot &S = H->slot[k % kHelpSlots];
+    const uint32_t want = (g << 16) | (k + 1u);
+    for (uint32_t spin = 0; spin < kSpinLimit; ++spin) {
+        uint32_t st = 0;  // 1 ready in the slot, 2 claimed by the owner
+        if (lane == 0) {
+            if (lds_ld(&S.tag) == want) {
+                st = 1;
+            } else {
+                const uint32_t nx = lds_ld(&H->next);
+                if (nx == ((g << 16) | k) && atomicCAS(&H->next, nx, nx + 1u) == nx) st = 2;
+            }
+        }
+        st = (uint32_t)__shfl((int)st, 0, 64);
+        if (st == 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            diff = S.diff[lane];
+            l = S.l[lane];
+            m = S.m[lane];
+            ok = (S.okm >> lane) & 1ull;
+            wave_sync();
+            if (lane == 0) lds_st(&H->consumed, k + 1u);
+            return true;
+        }
+        if (st == 2) {
+            if (lane == 0) lds_st(&H->consumed, k + 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    flag_fault(p, kFaultTailWait);  // a claimed chunk never arrived (a logic error)
+    return false;
+}
+
+// Owner: close the job -- no further claims; wait for the chunks already claimed (their
+// slots are written exactly once), then give the block's job slot back.
+__device__ void help_close(HelpCtl *H, int lane, const SearchParams &p) {
+    if (lane == 0) {
+        const uint32_t g = H->gen;
+        const uint32_t old = atomicExch(&H->next, (g << 16) | kHelpNone);
+        const uint32_t claimed = old & 0xFFFFu, from = H->consumed;
+        for (uint32_t j = from; j < claimed && claimed != kHelpNone; ++j) {
+            uint32_t spin = 0;
+            while (lds_ld(&H->slot[j % kHelpSlots].tag) != ((g << 16) | (j + 1u)) && ++spin < kSpinLimit)
+                __builtin_amdgcn_s_sleep(1);
+            if (spin >= kSpinLimit) flag_fault(p, kFaultTailWait);
+        }
+        lds_st(&H->owner, 0u);
+    }
+    wave_sync();
+}
+
+// Helper: after its last codeword, a wave decodes claimed chunks of its siblings' jobs
+// until every wave of the block is past its last codeword and no job is open.
+template <int M, int TMAX, bool TAB>
+__device__ void help_loop(HelpCtl *H, const SearchParams &p, const uint8_t *ex, const uint16_t *lg,
+                          const uint64_t *chien, const uint8_t *waves0, int wave_stride, int lane) {
+    constexpr int W = Prep<M, TMAX>::W;
+    Prep<M, TMAX> Q;
+    uint32_t mygen = 0xFFFFFFFFu, qnch = 0;
+    uint64_t qbase = 0;
+    int qt = 0;
+    const double *qap = nullptr;
+    for (uint32_t spin = 0; spin < kSpinLimit; ++spin) {
+        const uint32_t own = lds_ld(&H->owner);
+        if (own == 0u) {
+            if (lds_ld(&H->idle) >= (uint32_t)kWavesPerBlock) return;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const uint32_t nx = lds_ld(&H->next);
+        const uint32_t g = nx >> 16, j = nx & 0xFFFFu;
+        if (j == kHelpNone) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        if (g != mygen) {  // a new job: its decode state, re-checked against the generation
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                Q.S0[w] = H->S0[w];
+                Q.Lo[w] = H->Lo[w][lane];
+                Q.scol[w] = H->scol[w][lane];
+            }
+            Q.Plo.w[0] = H->Plo[lane];
+            Q.ordb = H->ordb[lane];
+            qbase = H->base;
+            qnch = H->nch;
+            qt = H->t;
+            qap = reinterpret_cast<const double *>(waves0 + (size_t)(own - 1u) * wave_stride) + Smem<M, TMAX>::NP;
+            wave_sync();
+            if ((lds_ld(&H->next) >> 16) != g) continue;
+            mygen = g;
+        }
+        if (j >= qnch || j >= lds_ld(&H->consumed) + (uint32_t)kHelpSlots) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint32_t won = 0;
+        if (lane == 0) won = atomicCAS(&H->next, nx, nx + 1u) == nx;
+        won = (uint32_t)__shfl((int)won, 0, 64);
+        if (!won) continue;
+        Mask<1> diff[1];
+        int m[1];
+        double l[1];
+        bool ok[1];
+        decode_chunks<M, TMAX, 1, TAB>(Q, qbase + 64ull * j, qt, ex, lg, chien, qap, p.tab, diff, m, l, ok);
+        HelpSlot &S = H->slot[j % kHelpSlots];
+        S.diff[lane] = diff[0].w[0];
+        S.l[lane] = l[0];
+        S.m[lane] = (uint8_t)m[0];
+        const uint64_t okm = ballot(ok[0]);
+        if (lane == 0) S.okm = okm;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        wave_sync();
+        if (lane == 0) lds_st(&S.tag, (g << 16) | (j + 1u));
+        spin = 0;
+    }
+}
+
 // ------------------------------------------------ wave-per-codeword search
 // 64 consecutive test patterns per step, acceptance in pattern order. A codeword still
 // running after p.chunk_limit steps finishes through the analytic tail (above) or is handed
@@ -1363,11 +1646,13 @@ template <int M, int TMAX, bool TAB, bool AN>
 __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const uint16_t *lg,
                                 const uint32_t *col, const uint64_t *chien, double *as,
                                 double *ap, uint8_t *ordl, uint32_t cw, int lane, AnWave *an,
-                                uint32_t item) {
+                                uint32_t item, HelpCtl *help, int wid) {
     constexpr int NW = Geo<M>::NW;
     // analytic tail: exact chunks end at an_stop, then the candidates decide the rest
     bool an_tried = false, an_exact = false;
     uint64_t an_stop = 0;
+    bool helped = false;  // the exact chunks below an_stop with the block's idle waves
+    uint64_t help_base = 0;
     (void)an_tried;
     // analytic-tail timing records (p.tail_diag, diagnostics only): cycles per phase
     uint64_t dg_t0 = 0, dg_t1 = 0, dg_t2 = 0, dg_t3 = 0, dg_stage = 0;
@@ -1393,6 +1678,12 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
                 d[5] = dg_mode;
                 d[6] = t4 - dg_t3;                            // split chunks + replay + outputs
                 d[7] = S.i_end;
+#ifdef BCHK_AN_PROF
+                // second half of the buffer: the enumeration's step-phase cycles
+                unsigned long long *q = p.tail_diag + (size_t)p.tail_diag_cap * 8 + (size_t)r * 8;
+                if (an)
+                    for (int i = 0; i < 8; ++i) q[i] = an->prof[i];
+#endif
             }
         }
     };
@@ -1460,6 +1751,10 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
                 if (plan.mode == 2) {
                     an_exact = true;
                     an_stop = plan.stop;
+                    if (help) {
+                        helped = help_open<M, TMAX>(help, P, base0, (uint32_t)((an_stop - base0) >> 6), p.t, wid, lane);
+                        help_base = base0;
+                    }
                 }
             }
             if (an_exact && base0 >= an_stop) {
@@ -1473,8 +1768,14 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         double l[G];
         bool ok[G];
         bool handed = false;
-        if (!hand_off)
-            decode_chunks<M, TMAX, G, TAB>(P, base0, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok);
+        if (!hand_off) {
+            bool got = false;
+            if constexpr (AN && G == 1 && an_capable<M, TMAX>()) {
+                if (helped && base0 < an_stop)
+                    got = help_take(help, (uint32_t)((base0 - help_base) >> 6), diff[0].w[0], l[0], m[0], ok[0], lane, p);
+            }
+            if (!got) decode_chunks<M, TMAX, G, TAB>(P, base0, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok);
+        }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const uint64_t base = base0 + 64ull * (uint64_t)g;
@@ -1545,6 +1846,7 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         }
         if (S.done) break;
     }
+    if (helped) help_close(help, lane, p);
     write_outputs<M, TMAX>(S, P, p, cw, lane);
     tail_record();
 }
@@ -1576,10 +1878,6 @@ __device__ __forceinline__ void wave_done(const SearchParams &p, int lane, uint3
 // tail, then stores the codeword; consumers restore empty slots), kEmptySlot once the
 // first pass has finished (its per-XCD done counts reach *in_total) and no ticket is left.
 // Every wait is bounded (a logic error ends the wave instead of hanging it).
-// A bounded wait ran out (a logic error: its codeword stays unfinished): tell the host.
-__device__ __forceinline__ void flag_fault(const SearchParams &p, uint32_t bit) {
-    if (p.fault) atomicOr(p.fault, bit);
-}
 
 __device__ uint32_t tail_dequeue(const SearchParams &p, uint32_t &item) {
     constexpr uint32_t kTailSpin = 1u << 24;  // ~1 s of polling: a guard against logic errors
@@ -1626,6 +1924,20 @@ __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) BCHK_SEARCH_ATTR
 kaneko_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
+    constexpr int WB0 = Smem<M, TMAX>::WAVE_BYTES, SB0 = WB0 + (AN ? an_bytes<M, TMAX>() : 0);
+    if constexpr (AN && an_capable<M, TMAX>()) {
+        if (p.an_help && threadIdx.x < 64) {  // the helper job control: no job, nobody idle
+            HelpCtl *h = reinterpret_cast<HelpCtl *>(smem + ((p.td.bytes + 15) & ~15u) + kWavesPerBlock * SB0);
+            if (threadIdx.x == 0) {
+                h->idle = 0u;
+                h->owner = 0u;
+                h->gen = 0u;
+                h->next = kHelpNone;
+                h->consumed = 0u;
+            }
+            if (threadIdx.x < kHelpSlots) h->slot[threadIdx.x].tag = 0u;
+        }
+    }
     __syncthreads();
     const uint8_t *ex = smem + p.td.off_exp;
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
@@ -1640,6 +1952,12 @@ kaneko_search_kernel(SearchParams p) {
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
     AnWave *an = (AN && an_capable<M, TMAX>()) ? reinterpret_cast<AnWave *>(wbase + WB) : nullptr;
+    // helper waves (analytic tail kernel): the block's job control after the wave slices
+    uint8_t *waves0 = smem + ((p.td.bytes + 15) & ~15u);
+    HelpCtl *help = nullptr;
+    if constexpr (AN && an_capable<M, TMAX>()) {
+        if (p.an_help) help = reinterpret_cast<HelpCtl *>(waves0 + kWavesPerBlock * SB);
+    }
     // Three sources of codewords -- the first pass's hand-offs as they come (the analytic
     // tail beside the first pass), grid-stride over the batch (no queue), or the work queue
     // left by the fast path (sub-queue x holds items x, x+8, ...; a wave drains its own
@@ -1653,8 +1971,10 @@ kaneko_search_kernel(SearchParams p) {
     uint32_t gs = blockIdx.x * kWavesPerBlock + wid;
     const uint32_t total = (!live && p.queue) ? *p.qcount : 0u;
     const uint32_t nfront = (!live && p.queue && p.qfront_n) ? *p.qfront_n : total;  // past it: the back
-    if (!live && p.queue && gs >= total) return;  // more waves than work
-    int x = xcc_id(), exhausted = 0;
+    // more waves than work: nothing to take (a helper wave of the tail kernel still helps)
+    const bool none = !live && p.queue && gs >= total;
+    if (none && !help) return;
+    int x = xcc_id(), exhausted = none ? 8 : 0;
     uint32_t ndone = 0;
     for (;;) {
         uint32_t cw = kEmptySlot, item = 0;
@@ -1684,10 +2004,16 @@ kaneko_search_kernel(SearchParams p) {
             cw = p.queue[qi];
         }
         if (cw < p.count)  // never otherwise: no access outside the batch
-            search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item);
+            search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item, help, wid);
         ++ndone;
     }
     wave_done(p, lane, ndone);
+    if constexpr (AN && an_capable<M, TMAX>()) {
+        if (help) {  // past its last codeword: help the siblings until all of them are
+            if (lane == 0) atomicAdd(&help->idle, 1u);
+            help_loop<M, TMAX, TAB>(help, p, ex, lg, chien, waves0, SB, lane);
+        }
+    }
 }
 
 // --------------------------------------- long codes: first patterns of every codeword
@@ -1771,7 +2097,6 @@ constexpr int kCoopSlotsMax = 64;
 template <int NW>
 constexpr int coop_slots() { return NW == 1 ? BCHK_COOP_SLOTS : 16; }
 static_assert(BCHK_COOP_SLOTS <= kCoopSlotsMax, "ring flags are polled one slot per lane");
-constexpr uint32_t kSpinLimit = 1u << 24;  // ~1 s of polling: a guard against logic errors
 
 template <int NW>
 struct CoopSlot {  // one decoded chunk
@@ -1792,18 +2117,6 @@ struct CoopCtl {
     uint32_t ready[kCoopSlotsMax];  // chunk index + 1 once the slot holds that chunk
 };
 
-__device__ __forceinline__ uint32_t lds_ld(const uint32_t *a) {
-    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st(uint32_t *a, uint32_t v) {
-    __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint64_t lds_ld64(const uint64_t *a) {
-    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st64(uint64_t *a, uint64_t v) {
-    __hip_atomic_store(a, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 __device__ __forceinline__ uint32_t exact_finished(const SearchParams &p) {
     uint32_t v = 0;
@@ -2290,6 +2603,7 @@ static KernelSet make_set() {
             k.tail_tab_ptr = &search_fn<M, TMAX, true, true>;
         }
         k.tail_wave_bytes = (size_t)(Smem<M, TMAX>::WAVE_BYTES + an_bytes<M, TMAX>());
+        k.tail_block_bytes = (size_t)help_bytes<M, TMAX>();
     }
     k.coop_bytes = coop;
     k.alg = &launch_alg_impl<M, TMAX>;

@@ -29,6 +29,7 @@ struct KernelSet {
     const void *(*tail_ptr)();
     const void *(*tail_tab_ptr)();
     size_t tail_wave_bytes;
+    size_t tail_block_bytes;  // the block's helper-job control (HelpCtl) after the waves
 };
 
 typedef hipError_t (*FastFn)(const SearchParams &, size_t, hipStream_t);

@@ -23,7 +23,8 @@ for J, snr, limit in cfgs:
     _, y, _ = d.generate(snr, 1 << 20, seed=1)
     d.decode(y)
     d.decode(y)
-    r = d.tail_diag(1 << 16).astype(np.uint64)
+    r = d.tail_diag(1 << 15).astype(np.uint64)
+    pf = d.tail_prof(len(r)).astype(np.int64) if "anprof" in os.environ.get("BCHK_LIB", "") else None
     cw = (r[:, 0] & np.uint64(0xFFFFFF)).astype(np.int64)
     xcd = ((r[:, 0] >> np.uint64(24)) & np.uint64(15)).astype(np.int64)
     start = (r[:, 0] >> np.uint64(28)).astype(np.int64)
@@ -62,4 +63,8 @@ for J, snr, limit in cfgs:
                         "setup": int(setup[i]), "iters": int(iters[i]), "mode": int(mode[i]),
                         "split": int(split[i]), "after": int(after[i]), "decodes": int(dec[i])}
                        for i in np.argsort(-tot)[:10]]}
+    if pf is not None:  # enumeration cycles by step phase (experiment build)
+        names = ["pop", "single", "leafrun", "push", "emits", "emit_cyc", "leaf_rounds", "steps"]
+        out["prof_sum"] = {k: int(v) for k, v in zip(names, pf.sum(axis=0))}
+        out["prof_slowest"] = [{k: int(v) for k, v in zip(names, pf[i])} for i in np.argsort(-tot)[:5]]
     print(json.dumps(out), flush=True)
