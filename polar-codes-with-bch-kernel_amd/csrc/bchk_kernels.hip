@@ -757,12 +757,14 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         const uint64_t idle = ballot(!have);
         const int nidle = __popcll(idle);
         const int take = nidle < sp ? nidle : sp;
-        if (!have) {
+        {   // every lane loads a slot (clamped) and the idle ones below `take` keep it: no
+            // exec-mask branch around the loads
             const int k = __popcll(idle & below);
-            if (k < take) {
-                nd = A->stack[sp - 1 - k];
-                have = true;
-            }
+            const int slot = sp - 1 - k;
+            const AnNode c = A->stack[slot > 0 ? slot : 0];
+            const bool tk = !have & (k < take);
+            if (tk) nd = c;
+            have = have | tk;
         }
         sp -= take;
         if (ballot(have) == 0ull) {  // done: emit what is still pending
@@ -790,14 +792,16 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         const uint32_t uq = A->ucls[qr];
         // the node carries its residual's class: no dependent load for the class mask
         const uint32_t cmk = A->cmask[cbits >= 0 ? nd.cls : 0];
+        // (flags combined with & and |, not && and ||: every operand is at hand, and the
+        // short-circuit forms compiled to exec-mask branches)
         const int64_t X = limfix - nd.sum;
-        const bool valid = have && next < NU && depth < t && aq <= X;
+        const bool valid = have & (next < NU) & (depth < t) & (aq <= X);
         const int64_t cs = nd.sum + aq;
-        const bool expand = valid && depth + 1 < t && q + 1 < NU && anext <= limfix - cs;
+        const bool expand = valid & (depth + 1 < t) & (q + 1 < NU) & (anext <= limfix - cs);
         // no child from q on can expand (the pair sums ascend): all of them are leaves, and
         // the ones whose residual matches are found from the class masks at once
-        const bool run = valid && !expand && cbits >= 0;
-        const bool single = valid && !run;
+        const bool run = valid & !expand & (cbits >= 0);
+        const bool single = valid & !run;
         // a single child (visited one per step)
         const uint64_t crem = nd.rem ^ rq;
         const uint32_t ccomb = nd.comb ^ cq;
@@ -832,7 +836,7 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
 #endif
             }
         };
-        push(single && crem == 0ull && (nkern > 0 || __popc(ccomb >> jb) <= t - depth - 1), csel, ccomb, cs);
+        push(single & (crem == 0ull) & ((nkern > 0) | (__popc(ccomb >> jb) <= t - depth - 1)), csel, ccomb, cs);
         drain();
         AN_PF(1)
         // a leaf run from q on: of the remaining children only those whose residual
@@ -858,15 +862,16 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
                 av[i] = A->afix[mi[i]];
                 cv[i] = A->cu[mi[i] < NU ? mi[i] : 0];
             }
-            bool stop = false;
-            uint32_t pm = 0u;  // elements to push
+            uint32_t alive = 1u, pm = 0u;  // below the bound so far; elements to push
+            const uint32_t anyk = nkern > 0 ? 1u : 0u;
 #pragma unroll
             for (int i = 0; i < kAnLeaf; ++i) {
-                stop = stop || !(av[i] <= X);  // the sentinel at NU never fits
+                alive &= av[i] <= X ? 1u : 0u;  // the sentinel at NU never fits
                 const uint32_t pc = nd.comb ^ cv[i];
-                if (!stop && (nkern > 0 || __popc(pc >> jb) <= t - depth - 1)) pm |= 1u << i;
+                const uint32_t pass = anyk | (__popc(pc >> jb) <= t - depth - 1 ? 1u : 0u);
+                pm |= (alive & pass) << i;
             }
-            if (stop) mm = 0u;
+            mm = alive ? mm : 0u;
             if (ballot(pm != 0u)) {
 #pragma unroll
                 for (int i = 0; i < kAnLeaf; ++i) {
@@ -877,7 +882,7 @@ __device__ int an_enumerate(AnWave *A, int NU, int t, int64_t limfix, uint64_t r
         }
         AN_PF(2)
         // the parent stays open iff its next child fits too
-        const bool cont = expand && anext <= X;
+        const bool cont = expand & (anext <= X);
         const uint64_t em = ballot(cont);
         const int cnt = __popcll(em);
         if (sp + cnt > kAnStack) {
