@@ -1293,9 +1293,17 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     for (int q = 0; q < t && q < NU; ++q) prefix_t += rdlf(P.asv[0], NB + q);
     const double hi = full < 2.0 * prefix_t ? full : 2.0 * prefix_t;
     const double delta = hi / 63.0;  // sums <= hi land in bins 0..63
-    uint32_t dp[TMAX + 1];
+    // counts by subset size w packed two per word (dp[2i] | dp[2i+1] << 16), saturating at
+    // 2^16 - 1: every budget compared below is < 2^16, so a saturated count decides the same
+    // (half the permutes and adds of 32-bit counts)
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    constexpr int NPK = (TMAX + 2) / 2;
+    uint32_t pk[NPK];
 #pragma unroll
-    for (int w = 0; w <= TMAX; ++w) dp[w] = (w == 0 && lane == 0) ? 1u : 0u;
+    for (int i = 0; i < NPK; ++i) pk[i] = (i == 0 && lane == 0) ? 1u : 0u;
+    uint32_t wmask[NPK];  // weights <= t
+#pragma unroll
+    for (int i = 0; i < NPK; ++i) wmask[i] = (2 * i <= t ? 0xFFFFu : 0u) | (2 * i + 1 <= t ? 0xFFFF0000u : 0u);
     // bin of every U element (lane NB + q), all at once
     int mybin = 64;
     {
@@ -1306,27 +1314,31 @@ __device__ AnPlan an_plan(const SearchState<1> &S, const Prep<M, TMAX> &P, const
     for (int q = 0; q < NU; ++q) {
         const int b = (int)rdl((uint32_t)mybin, NB + q);
         if (b >= 64) break;  // ascending: no later element fits a bin either
-        // every weight's shifted counts first (the permutes issue back to back), then the adds
-        uint32_t from[TMAX];
+        // every pair's shifted counts first (the permutes issue back to back), then the adds:
+        // size w gains the subsets of size w - 1 whose sum lies b bins lower
+        uint32_t sh[NPK];
         const int src = ((lane - b) & 63) << 2;
 #pragma unroll
-        for (int w = 1; w <= TMAX; ++w)
-            from[w - 1] = w <= t ? (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)dp[w - 1]) : 0u;
+        for (int i = 0; i < NPK; ++i) sh[i] = 2 * i < t ? (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pk[i]) : 0u;
 #pragma unroll
-        for (int w = 1; w <= TMAX; ++w) {
-            const uint32_t add = lane >= b ? from[w - 1] : 0u;
-            dp[w] = dp[w] + add < dp[w] ? 0xFFFFFFFFu : dp[w] + add;  // saturating
+        for (int i = 0; i < NPK; ++i) sh[i] = lane >= b ? sh[i] : 0u;
+#pragma unroll
+        for (int i = NPK - 1; i >= 0; --i) {
+            // (dp'[2i - 1], dp'[2i]) -> the pair (2i, 2i + 1)
+            const uint32_t add = __builtin_amdgcn_alignbit(sh[i], i > 0 ? sh[i - 1] : 0u, 16) & wmask[i];
+            const u16x2 r = __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, pk[i]), __builtin_bit_cast(u16x2, add));
+            pk[i] = __builtin_bit_cast(uint32_t, r);
         }
     }
-    uint32_t cnt = 0;
+    uint32_t cnt = 0;  // < 2^32: at most 64 bins x (TMAX + 1) counts of < 2^16
 #pragma unroll
-    for (int w = 0; w <= TMAX; ++w) cnt = cnt + dp[w] < cnt ? 0xFFFFFFFFu : cnt + dp[w];
+    for (int i = 0; i < NPK; ++i) cnt += (pk[i] & 0xFFFFu) + (pk[i] >> 16);
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {  // inclusive prefix over the bins
         const uint32_t x = (uint32_t)__shfl((int)cnt, (lane - o) & 63, 64);
-        const uint32_t add = lane >= o ? x : 0u;
-        cnt = cnt + add < cnt ? 0xFFFFFFFFu : cnt + add;
+        cnt += lane >= o ? x : 0u;
     }
+    static_assert(4 * kAnBudget < 0xFFFFu, "budgets compared against 16-bit saturated counts");
     if (p.tail_diag) plan.t_setup = (uint32_t)(__builtin_amdgcn_s_memtime() - t_0);
     uint32_t budget = kAnBudget;
     for (int attempt = 0; attempt < 2; ++attempt, budget *= 4) {
