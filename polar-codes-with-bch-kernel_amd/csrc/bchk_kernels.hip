@@ -173,11 +173,12 @@ __device__ __forceinline__ void prep_loaded(const SearchParams &p, const uint32_
         if (pos < N) ap[pos] = P.av[s];
     }
     wave_sync();
-    if constexpr (M >= 7) {
-        // long codes: sort the wave's 64 NW keys (f64 bits of |alpha| with the low 8
-        // mantissa bits replaced by the position) with a bitonic network. Keys whose 55-bit
-        // |alpha| prefixes all differ are ordered exactly as (|alpha|, position); a prefix tie
-        // between sorted neighbours -- an exact tie or a near one -- takes the exact rank below.
+    {
+        // sort the wave's 64 NW keys (f64 bits of |alpha| with the low 8 mantissa bits
+        // replaced by the position) with a bitonic network. Keys whose 55-bit |alpha|
+        // prefixes all differ are ordered exactly as (|alpha|, position); a prefix tie between
+        // sorted neighbours -- an exact tie or a near one -- takes the exact rank below. (Round
+        // 3: also for n <= 63, where the O(n^2) rank cost ~10 instructions per position.)
         uint64_t key[NW];
 #pragma unroll
         for (int s = 0; s < NW; ++s) {
