@@ -663,6 +663,12 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             q.heavy_big = hybrid ? c->tail_min_bound : 0;
             q.tail_rec = (TailRec *)P.l1rec.p;
         }
+        if (c->tail_diag_on && !inl) {  // experiment builds (BCHK_AN_PROF): first-pass phase cycles
+            if (!c->tdiag.p && (rc = c->tdiag.ensure(size_t(1) << 22))) return rc;
+            HIP_TRY(hipMemsetAsync(c->tdiag.p, 0, c->tdiag.cap, s));
+            q.tail_diag = (unsigned long long *)c->tdiag.p;
+            q.tail_diag_cap = (uint32_t)(c->tdiag.cap / 128);
+        }
         if (inl) {  // the analytic tail inside the first pass; failures to the cooperative kernel
             q.analytic = 1;
             q.tail_stats = ctrl + kTailStats;
@@ -708,7 +714,8 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
         }
         if (c->tail_diag_on) {
             if (!c->tdiag.p && (rc = c->tdiag.ensure(size_t(1) << 22))) return rc;
-            HIP_TRY(hipMemsetAsync(c->tdiag.p, 0, c->tdiag.cap, s));
+            if (inl)  // (otherwise zeroed before the first pass)
+                HIP_TRY(hipMemsetAsync(c->tdiag.p, 0, c->tdiag.cap, s));
             q.tail_diag = (unsigned long long *)c->tdiag.p;
             q.tail_diag_count = ctrl + kTailStats + 16;
             q.tail_diag_cap = (uint32_t)(c->tdiag.cap / 128);  // second half: bchk_tail_prof_read

@@ -1676,8 +1676,30 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     uint64_t dg_t0 = 0, dg_t1 = 0, dg_t2 = 0, dg_t3 = 0, dg_stage = 0;
     uint32_t dg_iters = 0, dg_mode = 0;
     if (AN && p.tail_diag) dg_t0 = __builtin_amdgcn_s_memtime();
+#ifdef BCHK_AN_PROF
+    // experiment builds: the first pass's cycles by phase, summed over its codewords into
+    // the last prof record of the tail diagnostics ([0] prep, [1] decode, [2] acceptance,
+    // [3] outputs, [4] chunks, [5] codewords)
+    uint64_t fq = __builtin_amdgcn_s_memtime(), fp[6] = {0, 0, 0, 0, 0, 1};
+#define FP_STAMP(i)                                         \
+    {                                                       \
+        const uint64_t tn_ = __builtin_amdgcn_s_memtime(); \
+        fp[i] += tn_ - fq;                                  \
+        fq = tn_;                                           \
+    }
+    auto fp_flush = [&]() {
+        if (!AN && p.tail_diag && lane == 0) {
+            unsigned long long *q = p.tail_diag + (size_t)p.tail_diag_cap * 8 + (size_t)(p.tail_diag_cap - 1) * 8;
+            for (int i = 0; i < 6; ++i) atomicAdd(q + i, (unsigned long long)fp[i]);
+        }
+    };
+#else
+#define FP_STAMP(i)
+    auto fp_flush = [&]() {};
+#endif
     Prep<M, TMAX> P;
     prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+    FP_STAMP(0)
     if (AN && p.tail_diag) dg_t1 = __builtin_amdgcn_s_memtime();
     SearchState<NW> S;
     init_state<M>(S, p.variant);
@@ -1794,6 +1816,10 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
             }
             if (!got) decode_chunks<M, TMAX, G, TAB>(P, base0, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok);
         }
+        FP_STAMP(1)
+#ifdef BCHK_AN_PROF
+        fp[4] += 1;
+#endif
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const uint64_t base = base0 + 64ull * (uint64_t)g;
@@ -1858,7 +1884,9 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
             }
             if (S.done) break;
         }
+        FP_STAMP(2)
         if (handed) {
+            fp_flush();
             tail_record();
             return;
         }
@@ -1866,6 +1894,9 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     }
     if (helped) help_close(help, lane, p);
     write_outputs<M, TMAX>(S, P, p, cw, lane);
+    FP_STAMP(3)
+    fp_flush();
+#undef FP_STAMP
     tail_record();
 }
 

@@ -24,6 +24,7 @@ for J, snr, limit in cfgs:
     d.decode(y)
     d.decode(y)
     r = d.tail_diag(1 << 15).astype(np.uint64)
+    r = r[:min(len(r), (1 << 15) - 1)]
     pf = d.tail_prof(len(r)).astype(np.int64) if "anprof" in os.environ.get("BCHK_LIB", "") else None
     cw = (r[:, 0] & np.uint64(0xFFFFFF)).astype(np.int64)
     xcd = ((r[:, 0] >> np.uint64(24)) & np.uint64(15)).astype(np.int64)
@@ -67,4 +68,6 @@ for J, snr, limit in cfgs:
         names = ["pop", "single", "leafrun", "push", "emits", "emit_cyc", "leaf_rounds", "steps"]
         out["prof_sum"] = {k: int(v) for k, v in zip(names, pf.sum(axis=0))}
         out["prof_slowest"] = [{k: int(v) for k, v in zip(names, pf[i])} for i in np.argsort(-tot)[:5]]
+        fp = d.tail_prof(1 << 15)[-1].astype(np.int64)  # the first pass, summed (last record)
+        out["first_pass"] = {k: int(v) for k, v in zip(["prep", "decode", "accept", "outputs", "chunks", "codewords"], fp[:6])}
     print(json.dumps(out), flush=True)
