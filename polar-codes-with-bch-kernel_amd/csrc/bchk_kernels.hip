@@ -479,9 +479,30 @@ __device__ __forceinline__ void accept_success(SearchState<Geo<M>::NW> &S, const
     }
 }
 
+// The sent word's positions lane + 64 s, loaded when the codeword's search starts (its
+// latency then hides under the search instead of the output step's).
+template <int NW>
+struct TxPre {
+    uint8_t v[NW];
+    bool valid;
+};
+template <int M>
+__device__ __forceinline__ TxPre<Geo<M>::NW> tx_prefetch(const SearchParams &p, uint32_t cw, int lane) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    TxPre<NW> t;
+    t.valid = p.cnt != nullptr;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const int pos = lane + 64 * s;
+        t.v[s] = (t.valid && pos < N) ? p.tx[(size_t)cw * N + pos] : (uint8_t)0;
+    }
+    return t;
+}
+
 template <int M, int TMAX>
 __device__ __forceinline__ void write_outputs(const SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
-                              const SearchParams &p, uint32_t cw, int lane) {
+                              const SearchParams &p, uint32_t cw, int lane,
+                              TxPre<Geo<M>::NW> txp = TxPre<Geo<M>::NW>{{}, false}) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
     const bool word_variant = p.variant == BCHK_VARIANT_WORD;
     const uint64_t decodes = S.i_end;
@@ -498,7 +519,10 @@ __device__ __forceinline__ void write_outputs(const SearchState<Geo<M>::NW> &S, 
         } else if (p.cnt && pos < N) {
             x = p.res[(size_t)cw * N + pos];  // not accepted: the row stays the caller's
         }
-        if (p.cnt) bit_errors += (uint32_t)__popcll(ballot(pos < N && x != p.tx[(size_t)cw * N + pos]));
+        if (p.cnt) {
+            const uint8_t tv = txp.valid ? txp.v[s] : (pos < N ? p.tx[(size_t)cw * N + pos] : (uint8_t)0);
+            bit_errors += (uint32_t)__popcll(ballot(pos < N && x != tv));
+        }
     }
     if (p.cnt && lane == 0) {  // src/dataForPlot.cpp:55-74
         unsigned long long *c = p.cnt + (size_t)(cw % (uint32_t)kCntSlots) * kCntStride;
@@ -1697,6 +1721,7 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
 #define FP_STAMP(i)
     auto fp_flush = [&]() {};
 #endif
+    const TxPre<NW> txp = tx_prefetch<M>(p, cw, lane);
     Prep<M, TMAX> P;
     prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
     FP_STAMP(0)
@@ -1733,7 +1758,7 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         if (!p.queue) {
             first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
             if (S.done) {
-                write_outputs<M, TMAX>(S, P, p, cw, lane);
+                write_outputs<M, TMAX>(S, P, p, cw, lane, txp);
                 return;
             }
         }
@@ -1893,7 +1918,7 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         if (S.done) break;
     }
     if (helped) help_close(help, lane, p);
-    write_outputs<M, TMAX>(S, P, p, cw, lane);
+    write_outputs<M, TMAX>(S, P, p, cw, lane, txp);
     FP_STAMP(3)
     fp_flush();
 #undef FP_STAMP

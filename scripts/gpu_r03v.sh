@@ -18,7 +18,7 @@ for l in open('$OUT/an_diag.jsonl'):
 show() { python3 -c "import json; d=json.loads(open('$1').read().strip().splitlines()[-1]); print('$1'.split('/')[-1], d['ms_per_step'], [(k['name'][:40], k['ms']) for k in d['kernels']]); [print(p['snr_db'], p['ms_per_step'], [k['ms'] for k in p['kernels']]) for p in d['points']]"; }
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 0 > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 show $OUT/bench.json
-for cl in 4 6; do
+for cl in ${CLS:-}; do
   BCHK_CHUNK_LIMIT=$cl timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 0 > $OUT/bench_cl$cl.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
   show $OUT/bench_cl$cl.json
 done
