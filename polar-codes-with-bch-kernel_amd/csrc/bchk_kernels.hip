@@ -2113,14 +2113,23 @@ kaneko_first_kernel(SearchParams p) {
     uint8_t *ordl = wbase + NP * 16;
     const uint32_t stride = gridDim.x * kWavesPerBlock;
     // the next codeword's row is loaded while this one is decoded (its latency hidden)
+    // (and its sent word, for the fused counters at the output step)
     double ynext[NW];
+    TxPre<NW> txnext{{}, false};
     uint32_t cw = blockIdx.x * kWavesPerBlock + wid;
-    if (cw < p.count) load_row<M>(p, cw, lane, ynext);
+    if (cw < p.count) {
+        load_row<M>(p, cw, lane, ynext);
+        txnext = tx_prefetch<M>(p, cw, lane);
+    }
     for (; cw < p.count; cw += stride) {
         double yv[NW];
 #pragma unroll
         for (int s = 0; s < NW; ++s) yv[s] = ynext[s];
-        if (cw + stride < p.count) load_row<M>(p, cw + stride, lane, ynext);
+        const TxPre<NW> txp = txnext;
+        if (cw + stride < p.count) {
+            load_row<M>(p, cw + stride, lane, ynext);
+            txnext = tx_prefetch<M>(p, cw + stride, lane);
+        }
 #if defined(BCHK_FIRST_CUT) && BCHK_FIRST_CUT == 1
         // experiment builds only (wrong results, timing of the phases): channel loads
         if (yv[0] + yv[NW - 1] == 12345.0) p.l0[cw] = 0.0;  // keeps the loads
@@ -2144,7 +2153,7 @@ kaneko_first_kernel(SearchParams p) {
         init_state<M>(S, p.variant);
         first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
         if (S.done) {
-            write_outputs<M, TMAX>(S, P, p, cw, lane);
+            write_outputs<M, TMAX>(S, P, p, cw, lane, txp);
         } else if (lane == 0) {
             p.queue_out[atomicAdd(p.qtail, 1u)] = cw;
         }
