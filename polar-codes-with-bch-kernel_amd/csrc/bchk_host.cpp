@@ -414,6 +414,7 @@ struct bchk_ctx {
     uint8_t *d_tables = nullptr;
     hipStream_t stream = nullptr;
     size_t lds = 0, lds_alg = 0, lds_tail = 0;
+    size_t lds_tab = 0;  // the first pass with the syndrome table: no Chien rows in LDS
     int grid = 0, grid_tab = 0, grid_tail = 0, grid_tail_tab = 0;
     uint64_t max_decodes = 0;
     DevBuf y, res, l0, st, words, synd, ok;
@@ -680,11 +681,12 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             q.heads = ctrl + 32;
             if (c->heavy_first && c->m <= 6) q.qfront_n = ctrl + kQFront;
             // every resident wave may take work; waves beyond the queue length exit at once
-            HIP_TRY(inl ? launch_tail(c->ks, q, igrid, c->lds_tail, s) : launch_search(c->ks, q, grid, c->lds, s));
+            HIP_TRY(inl ? launch_tail(c->ks, q, igrid, c->lds_tail, s)
+                        : launch_search(c->ks, q, grid, tabk ? c->lds_tab : c->lds, s));
         } else {
             const int need = (int)((B + kWavesPerBlock - 1) / kWavesPerBlock);
             HIP_TRY(inl ? launch_tail(c->ks, q, std::max(1, std::min(igrid, need)), c->lds_tail, s)
-                        : launch_search(c->ks, q, std::max(1, std::min(grid, need)), c->lds, s));
+                        : launch_search(c->ks, q, std::max(1, std::min(grid, need)), tabk ? c->lds_tab : c->lds, s));
         }
     }
     if (c->profile) HIP_TRY(hipEventRecord(ev.e[3], s));
@@ -861,6 +863,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     }
     const size_t tb = (c->td.bytes + 15) & ~size_t(15);
     c->lds = tb + kWavesPerBlock * c->ks.wave_bytes;
+    c->lds_tab = ((c->td.off_chien + 15) & ~size_t(15)) + kWavesPerBlock * c->ks.wave_bytes;
     c->lds_tail = tb + kWavesPerBlock * c->ks.tail_wave_bytes + c->ks.tail_block_bytes;
     c->lds_alg = tb;
     if (select_fast(m, t, &c->fast))  // m >= 7: kaneko_first_kernel, the search kernel's layout
@@ -905,7 +908,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     c->grid = grid_of(c->ks.search_ptr(), kWaveSize * kWavesPerBlock, c->lds);
     if (c->ks.search_tab) {
         c->grid_coop_tab = grid_of(c->ks.coop_tab_ptr(), kCoopThreads, c->lds_coop);
-        c->grid_tab = grid_of(c->ks.search_tab_ptr(), kWaveSize * kWavesPerBlock, c->lds);
+        c->grid_tab = grid_of(c->ks.search_tab_ptr(), kWaveSize * kWavesPerBlock, c->lds_tab);
     }
     if (c->ks.tail) c->grid_tail = grid_of(c->ks.tail_ptr(), kWaveSize * kWavesPerBlock, c->lds_tail);
     if (c->ks.tail_tab) c->grid_tail_tab = grid_of(c->ks.tail_tab_ptr(), kWaveSize * kWavesPerBlock, c->lds_tail);

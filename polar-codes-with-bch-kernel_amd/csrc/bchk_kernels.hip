@@ -1991,13 +1991,19 @@ __device__ uint32_t tail_dequeue(const SearchParams &p, uint32_t &item) {
 #ifdef BCHK_SEARCH_WPE
 #define BCHK_SEARCH_ATTR __attribute__((amdgpu_waves_per_eu(BCHK_SEARCH_WPE)))
 #else
-#define BCHK_SEARCH_ATTR __attribute__((amdgpu_waves_per_eu((TAB && !AN) ? 5 : 1)))
+#ifndef BCHK_FIRST_WPE
+#define BCHK_FIRST_WPE 5  // measured: 6 / 7 / 8 (spilling) are slower (profiles/r03_help/bench_fwpe*.json)
+#endif
+#define BCHK_SEARCH_ATTR __attribute__((amdgpu_waves_per_eu((TAB && !AN) ? BCHK_FIRST_WPE : 1)))
 #endif
 template <int M, int TMAX, bool TAB, bool AN>
 __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) BCHK_SEARCH_ATTR
 kaneko_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    load_tables(smem, p.tables, p.td.bytes);
+    // the first pass with the syndrome table never runs the Chien search: its tables stop
+    // before the Chien rows (the last table), which leaves LDS for more waves
+    const uint32_t tbytes = (TAB && !AN) ? p.td.off_chien : p.td.bytes;
+    load_tables(smem, p.tables, tbytes);
     constexpr int WB0 = Smem<M, TMAX>::WAVE_BYTES, SB0 = WB0 + (AN ? an_bytes<M, TMAX>() : 0);
     if constexpr (AN && an_capable<M, TMAX>()) {
         if (p.an_help && threadIdx.x < 64) {  // the helper job control: no job, nobody idle
@@ -2016,12 +2022,12 @@ kaneko_search_kernel(SearchParams p) {
     const uint8_t *ex = smem + p.td.off_exp;
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
     const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
-    const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
+    const uint64_t *chien = (TAB && !AN) ? nullptr : reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int NP = Smem<M, TMAX>::NP;
     // per wave: the prep's LDS slice, then the analytic tail's state (n <= 63)
     constexpr int WB = Smem<M, TMAX>::WAVE_BYTES, SB = WB + (AN ? an_bytes<M, TMAX>() : 0);
-    uint8_t *wbase = smem + ((p.td.bytes + 15) & ~15u) + wid * SB;
+    uint8_t *wbase = smem + ((tbytes + 15) & ~15u) + wid * SB;
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
