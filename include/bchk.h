@@ -227,8 +227,10 @@ int bchk_tail_stats(bchk_ctx *ctx, uint64_t *out6);
 int bchk_tail_diag_read(bchk_ctx *ctx, uint64_t *out, size_t items, uint64_t *count);
 /* Diagnostics of experiment builds (BCHK_AN_PROF, lib/libbchk_anprof.so): per record of
  * bchk_tail_diag_read, 8 u64 of enumeration cycles by step phase -- pops, loads and single
- * children, leaf runs, stack pushes, emission batches, their cycles, leaf-run rounds, steps
- * (zeros in the product build). */
+ * children, leaf runs, stack pushes, emission batches, their cycles, leaf-run rounds, steps;
+ * the record at index items - 1 of a 32768-record read holds the first pass's cycles summed
+ * over its codewords -- prep, decode, acceptance, outputs, chunks, codewords (zeros in the
+ * product build). */
 int bchk_tail_prof_read(bchk_ctx *ctx, uint64_t *out, size_t items);
 /* Enable (default) or disable the fast path; results are identical either way. */
 int bchk_set_fast_path(bchk_ctx *ctx, int enable);
