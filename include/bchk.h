@@ -159,9 +159,11 @@ int bchk_sweep_range(bchk_ctx *ctx, double snr_db, uint64_t *rng_state, uint64_t
  * src/bchCoder.cpp:236-240, redrawn only for the two largest engine values) and polar-method
  * attempts of four draws until ceil(n/2) pairs are accepted (normal_distribution, :243-250).
  * bchk_stream_skip: the engine state and draws after `words` words from `state` (no samples).
- * bchk_stream_sync: from a word start `state`, the first word start at or after `offset` draws
- * on the stream's own parse, found WITHOUT parsing the draws before `offset` (every parse
- * state possible at `offset` is followed until they merge; a redrawn information bit before
+ * bchk_stream_sync: from a word start `state`, a word start in [offset, offset + limit) draws
+ * on the stream's own parse that depends only on (state, offset, limit) -- the start where
+ * every parse state possible at `offset` has merged, not necessarily the first start at or
+ * after `offset` -- found WITHOUT parsing the draws before `offset` (neighbouring ranks make
+ * the identical call for a shared boundary, so parts tile the stream; a redrawn information bit before
  * `offset`, or no merge before offset + limit, returns 1 = unresolved): *word_offset (draws
  * from `state`) and *word_state. */
 int bchk_stream_skip(int k, int n, uint64_t state, uint64_t words, uint64_t *state_out, uint64_t *draws);

@@ -410,16 +410,171 @@ __device__ __forceinline__ bool alg_core_valu(const uint64_t *__restrict__ chien
     return ok;
 }
 
-// The decoder a kernel uses: VALU BM for m <= 6 unless BCHK_GF_LDS is defined.
+// ---------------------------------------------------------------------------
+// Long codes (m >= 7): the root test without the Chien scan.
+// Decoder::locatorsAndRoots (src/Decoder.cpp:279-296) accepts iff lambda has deg distinct
+// roots among alpha^0 .. alpha^(n-1), i.e. iff lambda splits into distinct linear factors
+// over GF(2^m)* -- iff lambda divides x^(2^m) - x = prod_a (x - a) (square-free; a = 0 is
+// excluded because lambda(0) = C_0 != 0: the inversionless BM multiplies C_0 = 1 by nonzero
+// discrepancies only). The scan costs n (t + 1) table lookups per test word (4080 at
+// BCH(255,139,31)); x^(2^m) mod lambda costs about (m - 4) (t + 1)^2 (~1 100 there), and a
+// failing word -- nearly every test pattern of a heavy codeword -- needs nothing more.
+// Registers are indexed by compile-time constants only, so the arithmetic is modulo the
+// reversed locator rho(x) = x^TMAX lambda(1/x) = sum_i C_i x^(TMAX - i), whose degree is
+// TMAX whatever deg lambda is (leading coefficient C_0): rho = x^s lambda_rev with
+// s = TMAX - deg, and lambda_rev (roots 1/X) divides x^(2^m) - x iff
+// x^(2^m + s) == x^(1 + s) (mod rho). Checked against the root count on random and split
+// locators for m = 7, 8 and every TMAX bucket (scripts/proto_m8_skip.c's companion
+// experiment, and the GPU parity tests through the exhaustive/random decoder tables).
+//
+// x g mod rho-hat (rho / C_0, monic: x^TMAX = sum_j q_j x^j), g linear, lq = log q
+template <int M, int TMAX>
+__device__ __forceinline__ void mulx_mod(const uint8_t *__restrict__ ex, const uint16_t *__restrict__ lg,
+                                         const int (&lq)[TMAX], uint32_t (&g)[TMAX]) {
+    const int lt = lg[g[TMAX - 1]];
+#pragma unroll
+    for (int j = TMAX - 1; j >= 0; --j) g[j] = (j ? g[j - 1] : 0u) ^ gf_exp2<M>(ex, lt, lq[j]);
+}
+// g^2 mod rho-hat: squares of the coefficients (Frobenius), then the top-down reduction of
+// degrees 2 TMAX - 2 .. TMAX
+template <int M, int TMAX>
+__device__ __forceinline__ void sqr_mod(const uint8_t *__restrict__ ex, const uint16_t *__restrict__ lg,
+                                        const int (&lq)[TMAX], uint32_t (&g)[TMAX]) {
+    uint32_t sq[2 * TMAX - 1];
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) {
+        const int l = lg[g[j]];
+        sq[2 * j] = gf_exp2<M>(ex, l, l);
+        if (j + 1 < TMAX) sq[2 * j + 1] = 0u;
+    }
+#pragma unroll
+    for (int k = 2 * TMAX - 2; k >= TMAX; --k) {
+        const int lk = lg[sq[k]];
+#pragma unroll
+        for (int j = 0; j < TMAX; ++j) sq[k - TMAX + j] ^= gf_exp2<M>(ex, lk, lq[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) g[j] = sq[j];
+}
+constexpr int floor_pow2(int v) { return v < 2 ? 1 : 2 * floor_pow2(v / 2); }
+constexpr int ilog2c(int v) { return v < 2 ? 0 : 1 + ilog2c(v / 2); }
+
+// lambda = C (logs lc), deg >= 1, C_0 != 0: true iff lambda has deg distinct roots in GF(2^m)*
+// (lanes with act = false give an unspecified answer)
+template <int M, int TMAX>
+__device__ __forceinline__ bool split_test(const uint8_t *__restrict__ ex, const uint16_t *__restrict__ lg,
+                                           const int (&lc)[TMAX + 1], int deg, bool act) {
+    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL;
+    static_assert(TMAX >= 2, "split test needs TMAX >= 2");
+    int lq[TMAX];
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) {  // q_j = C_(TMAX - j) / C_0
+        const int v = lc[TMAX - j];
+        int d = v - lc[0];
+        d = d < 0 ? d + N : d;
+        lq[j] = v == ZL ? ZL : d;
+    }
+    // x^(2P) for the largest power of two P <= TMAX - 1 (so 2P >= TMAX): x^TMAX = q, then
+    // 2P - TMAX multiplications by x; then squarings up to x^(2^m)
+    constexpr int P = floor_pow2(TMAX - 1);
+    constexpr int SQ = M - ilog2c(2 * P);
+    static_assert(SQ >= 1, "2P < 2^m");
+    uint32_t g[TMAX];
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) g[j] = gf_exp2<M>(ex, lq[j], 0);
+#pragma unroll
+    for (int e = TMAX; e < 2 * P; ++e) mulx_mod<M, TMAX>(ex, lg, lq, g);
+#pragma unroll
+    for (int s = 0; s < SQ; ++s) sqr_mod<M, TMAX>(ex, lg, lq, g);
+    // times x^s, s = TMAX - deg (per lane; the wave runs the largest s of its active lanes)
+    const int sh = (act && deg >= 2) ? TMAX - deg : 0;
+    for (int st = 0; ballot(st < sh); ++st) {
+        uint32_t h[TMAX];
+#pragma unroll
+        for (int j = 0; j < TMAX; ++j) h[j] = g[j];
+        mulx_mod<M, TMAX>(ex, lg, lq, h);
+#pragma unroll
+        for (int j = 0; j < TMAX; ++j) g[j] = st < sh ? h[j] : g[j];
+    }
+    bool eq = true;
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) eq = eq && (g[j] == (j == 1 + sh ? 1u : 0u));
+    return deg == 1 || eq;  // a linear lambda with lambda(0) != 0 has its one root in GF*
+}
+
+// Decoder::decode for m >= 7, one test word per lane (wave-collective: every lane of the
+// wave must call it): BM (bm_locator), the split test, and for the lanes that pass -- rare
+// among test patterns -- the positions by a Chien scan spread over the wave (lane l tests
+// positions l + 64 s, as alg_decode_wave), one scan per successful lane. Same decision and
+// flipped positions as alg_core. Lanes with act = false report failure without the tests
+// (the caller knows their outcome cannot matter).
+template <int M, int TMAX>
+__device__ __forceinline__ bool alg_decode_lanes(const uint8_t *__restrict__ ex,
+                                                 const uint16_t *__restrict__ lg, const uint32_t *Sw,
+                                                 int t, Mask<Geo<M>::NW> &E, bool act = true) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    const int lane = (int)__lane_id();
+    uint32_t C[TMAX + 1];
+    int L;
+    bm_locator<M, TMAX>(ex, lg, Sw, t, C, L);
+    int deg = 0;
+#pragma unroll
+    for (int i = 1; i <= TMAX; ++i) deg = C[i] ? i : deg;
+    int lc[TMAX + 1];
+#pragma unroll
+    for (int i = 0; i <= TMAX; ++i) lc[i] = lg[C[i]];
+    bool ok = act && (L <= t) && (deg >= 1);
+    if (ballot(ok)) ok = split_test<M, TMAX>(ex, lg, lc, deg, ok) && ok;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) E.w[s] = 0;
+    for (uint64_t sm = ballot(ok); sm; sm &= sm - 1) {
+        const int src = (int)__builtin_ctzll(sm);
+        const int dg = uni(__shfl(deg, src, 64));
+        int kk[NW], ik[NW];
+        uint32_t v[NW];
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            const int pos = lane + 64 * s;
+            kk[s] = pos ? N - pos : 0;  // lambda(alpha^k) at k = (n - pos) mod n (:287)
+            ik[s] = 0;
+            v[s] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i <= TMAX; ++i) {
+            if (i <= dg) {
+                const int lti = __builtin_amdgcn_readlane(lc[i], src);
+#pragma unroll
+                for (int s = 0; s < NW; ++s) {
+                    v[s] ^= gf_exp2<M>(ex, lti, ik[s]);
+                    ik[s] += kk[s];
+                    ik[s] = ik[s] >= N ? ik[s] - N : ik[s];
+                }
+            }
+        }
+        int cnt = 0;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            const uint64_t r = ballot(lane + 64 * s < N && v[s] == 0u);
+            cnt += __popcll(r);
+            if (lane == src) E.w[s] = r;
+        }
+        if (lane == src && cnt != dg) ok = false;  // never: the split test said deg roots
+    }
+    return ok;
+}
+
+// The decoder a kernel uses: VALU BM for m <= 6 unless BCHK_GF_LDS is defined; m >= 7 the
+// split test (wave-collective).
 template <int M, int TMAX>
 __device__ __forceinline__ bool alg_decode_word(const uint8_t *ex, const uint16_t *lg,
                                                 const uint64_t *chien, const uint32_t *Sw, int t,
-                                                Mask<Geo<M>::NW> &E) {
+                                                Mask<Geo<M>::NW> &E, bool act = true) {
 #ifndef BCHK_GF_LDS
     if constexpr (M <= 6) return alg_core_valu<M, TMAX>(chien, Sw, t, E);
     else
 #endif
-        return alg_core<M, TMAX>(ex, lg, chien, Sw, t, E);
+    if constexpr (M >= 7) return alg_decode_lanes<M, TMAX>(ex, lg, Sw, t, E, act);
+    else return alg_core<M, TMAX>(ex, lg, chien, Sw, t, E);
 }
 
 // Decoder::decode of ONE test word by a whole wave (its syndromes Sw wave-uniform): the

@@ -287,18 +287,50 @@ __device__ __forceinline__ void prep_syndromes(const uint32_t *col, int lane, Pr
     }
 }
 
+// The best codeword so far as a skip key: bit 63 valid, bits 32..39 u = its differences
+// from the hard decision outside the NB <= 31 least reliable positions, bits 0..30 dR = its
+// differences on them (bit b: sorted position b, the bit test pattern i flips, :36-51).
+template <int M, int TMAX>
+__device__ __forceinline__ uint64_t skip_key(const Mask<Geo<M>::NW> &best, const Prep<M, TMAX> &P, int lane) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    constexpr int NB = N < 31 ? N : 31;
+    const int op = P.ordb;  // lane b: position of sorted rank b
+    uint64_t dw = 0;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) dw = (u == (op >> 6)) ? best.w[u] : dw;
+    const uint32_t dR = (uint32_t)ballot(lane < NB && ((dw >> (op & 63)) & 1ull));
+    const int u = mask_popc<NW>(best) - __popc(dR);
+    return (1ull << 63) | ((uint64_t)(u > 255 ? 255 : u) << 32) | dR;
+}
+// pattern i re-finds the key's codeword (distance <= t): |D ^ P_i| = u + popc(dR ^ i)
+__device__ __forceinline__ bool skip_lane(uint64_t skey, uint64_t i, int t) {
+    const int u = (int)((skey >> 32) & 0xFFu);
+    const uint32_t dR = (uint32_t)skey & 0x7FFFFFFFu;
+    return (skey >> 63) && u + __popc(dR ^ ((uint32_t)i & 0x7FFFFFFFu)) <= t;
+}
+
 // Decode test patterns i = base + lane (base a multiple of 64) of G consecutive chunks
 // (bases base, base + 64, ...): success and diff = yH ^ x (flipped pattern positions ^
 // error locations); for successful lanes also m = calcM (:89-97) and l = calcL (:69-77),
 // summed over diff in index order from the wave's |alpha|-by-position LDS slice
 // (lane-parallel; the ordered acceptance only compares them). With the syndrome table the
 // G lookups are issued together, so a wave has G bucket loads in flight.
+//
+// Long codes: a pattern whose word lies within distance t of a codeword found at an EARLIER
+// pattern decodes to that codeword again (unique decoding, d >= 2t + 1; at distance 0 it
+// fails) and cannot be an improvement, since l0 <= its l from then on; nothing else in the
+// reference loop depends on a non-improving success (m0 only matters at an improvement,
+// where :374 re-reads it). skey (skip_key) describes the best codeword so far; such
+// patterns are reported as failures without decoding them -- same acceptance, same
+// counters. At 5 dB on BCH(255,139,31) a third of a heavy codeword's patterns re-find its
+// best codeword.
 template <int M, int TMAX, int G, bool TAB>
 __device__ __forceinline__ void decode_chunks(const Prep<M, TMAX> &P, uint64_t base, int t,
                                               const uint8_t *ex, const uint16_t *lg,
                                               const uint64_t *chien, const double *ap,
                                               const SyndTable &T, Mask<Geo<M>::NW> (&diff)[G],
-                                              int (&m)[G], double (&l)[G], bool (&ok)[G]) {
+                                              int (&m)[G], double (&l)[G], bool (&ok)[G],
+                                              uint64_t skey = 0) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
     constexpr int NB = N < 31 ? N : 31;
     uint32_t Sw[G][W];
@@ -333,7 +365,11 @@ __device__ __forceinline__ void decode_chunks(const Prep<M, TMAX> &P, uint64_t b
         for (int g = 0; g < G; ++g) ok[g] = tab_finish<M, TMAX>(T, K[g], H[g], B[g], E[g].w[0]);
     } else {
 #pragma unroll
-        for (int g = 0; g < G; ++g) ok[g] = alg_decode_word<M, TMAX>(ex, lg, chien, Sw[g], t, E[g]);
+        for (int g = 0; g < G; ++g) {
+            bool act = true;
+            if constexpr (M >= 7) act = !skip_lane(skey, base + 64ull * (uint64_t)g + (uint64_t)(__lane_id()), t);
+            ok[g] = alg_decode_word<M, TMAX>(ex, lg, chien, Sw[g], t, E[g], act);
+        }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -1506,7 +1542,8 @@ struct HelpCtl {
     uint32_t consumed;  // chunks the owner has taken, in order
     uint32_t nch;       // chunks in the job
     uint64_t base;      // first test pattern of chunk 0
-    int32_t t, pad;
+    int32_t t;
+    uint32_t jown;      // wave id + 1 of the job's owner, part of the job state (read with it)
     uint32_t S0[2];
     uint32_t Lo[2][64], scol[2][64];
     uint64_t Plo[64];
@@ -1548,6 +1585,7 @@ __device__ bool help_open(HelpCtl *H, const Prep<M, TMAX> &P, uint64_t base, uin
         H->base = base;
         H->nch = nch;
         H->t = t;
+        H->jown = (uint32_t)wid + 1u;
         H->consumed = 0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1649,7 +1687,12 @@ __device__ void help_loop(HelpCtl *H, const SearchParams &p, const uint8_t *ex, 
             qbase = H->base;
             qnch = H->nch;
             qt = H->t;
-            qap = reinterpret_cast<const double *>(waves0 + (size_t)(own - 1u) * wave_stride) + Smem<M, TMAX>::NP;
+            // the owner's |alpha| slice from the job state, not from `owner` (read before
+            // `next`: the job may have changed hands in between); the generation re-check
+            // below covers everything read here
+            const uint32_t jo = H->jown;
+            qap = reinterpret_cast<const double *>(waves0 + (size_t)((jo ? jo : 1u) - 1u) * wave_stride) +
+                  Smem<M, TMAX>::NP;
             wave_sync();
             if ((lds_ld(&H->next) >> 16) != g) continue;
             mygen = g;
@@ -1839,7 +1882,10 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
                 if (helped && base0 < an_stop)
                     got = help_take(help, (uint32_t)((base0 - help_base) >> 6), diff[0].w[0], l[0], m[0], ok[0], lane, p);
             }
-            if (!got) decode_chunks<M, TMAX, G, TAB>(P, base0, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok);
+            if (!got) {
+                const uint64_t skey = (M >= 7 && S.accepted) ? skip_key<M, TMAX>(S.best, P, lane) : 0ull;
+                decode_chunks<M, TMAX, G, TAB>(P, base0, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok, skey);
+            }
         }
         FP_STAMP(1)
 #ifdef BCHK_AN_PROF
@@ -2203,6 +2249,7 @@ struct CoopCtl {
     uint32_t drec;      // diagnostic builds: its record index
     uint64_t bound;     // the acceptor's current loop bound (diagnostics; may rise again)
     double l0;          // current l0 (monotone non-increasing)
+    uint64_t skey;      // skip_key of the best codeword so far (0: none yet)
     uint32_t ready[kCoopSlotsMax];  // chunk index + 1 once the slot holds that chunk
 };
 
@@ -2319,6 +2366,7 @@ kaneko_coop_kernel(SearchParams p) {
         if (threadIdx.x == 0) {
             ctl->bound = S.bound;
             ctl->l0 = S.l0;
+            ctl->skey = 0ull;
         }
         __syncthreads();
 #ifdef BCHK_DIAG
@@ -2346,11 +2394,14 @@ kaneko_coop_kernel(SearchParams p) {
                 if (stop) break;
                 const double l0r = __longlong_as_double((long long)lds_ld64(
                     reinterpret_cast<const uint64_t *>(&ctl->l0)));
+                // any published key is a codeword found in a chunk the acceptor has consumed,
+                // i.e. before chunk c (consumed <= c: chunk c is not decoded yet)
+                const uint64_t skey = M >= 7 ? lds_ld64(&ctl->skey) : 0ull;
                 Mask<NW> diff[G];
                 int m[G];
                 double l[G];
                 bool ok[G];
-                decode_chunks<M, TMAX, G, TAB>(P, base, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok);
+                decode_chunks<M, TMAX, G, TAB>(P, base, p.t, ex, lg, chien, ap, p.tab, diff, m, l, ok, skey);
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     const uint32_t cg = c + (uint32_t)g;
@@ -2456,10 +2507,12 @@ kaneko_coop_kernel(SearchParams p) {
                     if (S.done) { cdone = cc + 1u; break; }
                 }
                 c = cdone;
+                const uint64_t skey = (M >= 7 && S.accepted) ? skip_key<M, TMAX>(S.best, P, lane) : 0ull;
                 if (lane == 0) {
                     lds_st64(&ctl->bound, S.bound);
                     lds_st64(reinterpret_cast<uint64_t *>(&ctl->l0),
                              (uint64_t)__double_as_longlong(S.l0));
+                    if (M >= 7) lds_st64(&ctl->skey, skey);
                     lds_st(&ctl->consumed, c);
                 }
 #ifdef BCHK_DIAG
@@ -2660,7 +2713,9 @@ static hipError_t launch_first_impl(const SearchParams &p, size_t lds, hipStream
 bool select_first_long(int m, int t, FastFn *out) {
 #define BCHK_FIRST(MM, TT) \
     if (m == MM && t <= TT) { *out = &launch_first_impl<MM, TT>; return true; }
-#ifndef BCHK_ISA_ONLY
+#if defined(BCHK_ISA_ONLY) && BCHK_ISA_ONLY == 8
+    BCHK_FIRST(8, 15)
+#elif !defined(BCHK_ISA_ONLY)
     BCHK_FIRST(7, 8) BCHK_FIRST(7, 16) BCHK_FIRST(7, 32)
     BCHK_FIRST(8, 15) BCHK_FIRST(8, 16) BCHK_FIRST(8, 32)
 #endif
@@ -2705,7 +2760,9 @@ static KernelSet make_set() {
 bool select_kernels(int m, int t, KernelSet *out) {
 #define BCHK_TRY(MM, TT) \
     if (m == MM && t <= TT) { *out = make_set<MM, TT>(); return true; }
-#ifdef BCHK_ISA_ONLY  // ISA inspection builds: the headline code's kernels only
+#if defined(BCHK_ISA_ONLY) && BCHK_ISA_ONLY == 8  // ISA inspection builds: one code's kernels only
+    BCHK_TRY(8, 15)
+#elif defined(BCHK_ISA_ONLY)
     BCHK_TRY(6, 6)
 #else
     BCHK_TRY(2, 1)

@@ -78,7 +78,8 @@ inline int tab_kbits(int m, int t) {
 // a slot: t fields of m bits | tag = occupied bit | quotient (kbits - bbits) | distance (3)
 inline int tab_tbits(int m, int t, int bbits) { return 1 + (tab_kbits(m, t) - bbits) + kTabDistBits; }
 inline bool tab_fits(int m, int t, int bbits) {
-    return tab_tbits(m, t, bbits) <= 32 && tab_tbits(m, t, bbits) + m * t <= 64;
+    // < 32: tab_finish masks the tag with (1u << tbits) - 1u
+    return tab_tbits(m, t, bbits) < 32 && tab_tbits(m, t, bbits) + m * t <= 64;
 }
 constexpr int kTabMaxBucketBits = 20;  // 64 MiB
 inline bool syndtab_feasible(int m, int t) {  // n <= 63: one u64 mask; a layout within 64 MiB
