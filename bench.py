@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="reference processes for the CPU baseline (0 = the host's core share)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: the "
+                         "same exchange staged through the host, e.g. several ranks on one GPU)")
     ap.add_argument("--unfused", action="store_true",
                     help="decode_device + count_device (re-reads res and stats) instead of the fused call")
     return ap.parse_args()
@@ -285,7 +288,7 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
         "snr_db": snr, "value": value, "ms_per_step": elapsed / args.steps * 1e3,
         "fer": (int(cnt[0]) / words) if words else None,
         "ber": (int(cnt[1]) / words / n) if words else None,
-        "frame_errors": int(cnt[0]), "words": words,
+        "frame_errors": int(cnt[0]), "words": words, "counters": [int(c) for c in cnt],
         "decodes_per_codeword": (int(cnt[2]) / words) if words else None,
         "kernels": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in kk.items()} for kk in kern],
         "dominant_kernel": dom["name"], "dominant_GB_s": dom["GB_s"],
@@ -307,12 +310,18 @@ def main():
     import torch.distributed as dist
 
     bchk = load_pkg()
-    torch.cuda.set_device(local)
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the N > 1 path on one GPU, gloo)
+    # share them round-robin
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dec = bchk.KanekoKernelProcessor(args.m, args.t, J=args.J, device=local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    dec = bchk.KanekoKernelProcessor(args.m, args.t, J=args.J, device=gpu)
     n, B = dec.n, args.batch
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", gpu)
     snrs = [float(x) for x in args.points.split(",") if x.strip()] if args.points else []
     if args.snr not in snrs:
         snrs.append(args.snr)
@@ -352,7 +361,8 @@ def main():
                                    f"Eb/N0={args.snr} dB, J={'inf' if args.J < 0 else args.J}",
                        "code": f"BCH({n},{dec.k},{2 * args.t + 1})", "batch_per_gpu": B,
                        "global_batch": world * B, "snr_db": args.snr, "J": args.J,
-                       "L_inert": 8, "parallelism": f"dp{world}"},
+                       "L_inert": 8, "parallelism": f"dp{world}",
+                       "backend": args.backend if world > 1 else None},
             "fer": head["fer"],
             "ber": head["ber"],
             "decodes_per_codeword": head["decodes_per_codeword"],
@@ -365,7 +375,7 @@ def main():
             "points": [{"snr_db": p["snr_db"], "value": round(p["value"], 3),
                         "ms_per_step": round(p["ms_per_step"], 4), "fer": p["fer"],
                         "frame_errors": p["frame_errors"], "words": p["words"],
-                        "decodes_per_codeword": p["decodes_per_codeword"],
+                        "counters": p["counters"], "decodes_per_codeword": p["decodes_per_codeword"],
                         "dominant_kernel": p["dominant_kernel"], "frac": round(p["frac"], 6),
                         "kernels": p["kernels"], "tail": p["tail"]} for p in pts.values()],
             "tail": head["tail"],

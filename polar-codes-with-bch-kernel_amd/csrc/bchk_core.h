@@ -84,6 +84,11 @@ __device__ __forceinline__ uint64_t lane_xor64(uint64_t v, int lane) {
     return ((uint64_t)lane_xor<J>((uint32_t)(v >> 32), lane) << 32) | lane_xor<J>((uint32_t)v, lane);
 }
 
+// v of lane - 1 (DPP wave_shr:1); lane 0 gets `fill`
+__device__ __forceinline__ int wave_shr1(int v, int fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xF, 0xF, false);
+}
+
 // XOR over the wave
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
     const int lane = (int)__lane_id();
@@ -96,20 +101,43 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
     return v;
 }
 
+// f64 sum over the wave by recursive doubling (each lane's rounding order differs: callers
+// that branch on it take one lane's value)
+__device__ __forceinline__ double wave_sum_f64(double v) {
+    const int lane = (int)__lane_id();
+    uint64_t b = (uint64_t)__double_as_longlong(v);
+    b = (uint64_t)__double_as_longlong(__longlong_as_double((long long)b) +
+                                       __longlong_as_double((long long)lane_xor64<32>(b, lane)));
+    b = (uint64_t)__double_as_longlong(__longlong_as_double((long long)b) +
+                                       __longlong_as_double((long long)lane_xor64<16>(b, lane)));
+    b = (uint64_t)__double_as_longlong(__longlong_as_double((long long)b) +
+                                       __longlong_as_double((long long)lane_xor64<8>(b, lane)));
+    b = (uint64_t)__double_as_longlong(__longlong_as_double((long long)b) +
+                                       __longlong_as_double((long long)lane_xor64<4>(b, lane)));
+    b = (uint64_t)__double_as_longlong(__longlong_as_double((long long)b) +
+                                       __longlong_as_double((long long)lane_xor64<2>(b, lane)));
+    b = (uint64_t)__double_as_longlong(__longlong_as_double((long long)b) +
+                                       __longlong_as_double((long long)lane_xor64<1>(b, lane)));
+    return __longlong_as_double((long long)b);
+}
+
 __device__ __forceinline__ int xcc_id() {
     unsigned v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
     return (int)(v & 7u);
 }
 
-// alpha^(la + lb) with log(0) = ZL = 2n-1: the sum is clamped to ZL so the exp table has
-// 2n entries (exp[2n-1] = 0) -- at most 32 dwords for n <= 63, one per LDS bank, so
-// byte lookups from 32 lanes never conflict.
+// alpha^(la + lb) with log(0) = ZL = 2n-1 (la, lb in [0, n) or ZL). m <= 6: the sum is
+// clamped to ZL so the exp table has 2n entries (exp[2n-1] = 0) -- at most 32 dwords for
+// n <= 63, one per LDS bank, so byte lookups from 32 lanes never conflict. m >= 7: the table
+// has 4n entries, zero from 2n-1 on (bchk_host.cpp make_tables), so no clamp: one add per
+// product, in the decoders' innermost loops.
 template <int M>
 __device__ __forceinline__ uint32_t gf_exp2(const uint8_t *ex, int la, int lb) {
     constexpr int ZL = 2 * ((1 << M) - 1) - 1;
     const int s = la + lb;
-    return ex[s < ZL ? s : ZL];
+    if constexpr (M >= 7) return ex[s];
+    else return ex[s < ZL ? s : ZL];
 }
 
 template <int NW>
@@ -131,8 +159,12 @@ __device__ __forceinline__ int mask_popc(const Mask<NW> &m) {
 // syndromes Sw (byte j = S_{2j+1}). Success iff the syndrome is nonzero, the BM register
 // length L <= t and the locator has deg C >= 1 distinct roots in GF(2^m)*; E = flipped
 // positions ((n - k) mod n for each root alpha^k, :287).
-// Inversionless binary Berlekamp-Massey over the table GF(2^m): connection polynomial C
-// (TMAX + 1 coefficients) and register length L of the syndromes S_1 .. S_2t.
+// Binary Berlekamp-Massey over the table GF(2^m): connection polynomial C (TMAX + 1
+// coefficients, C_0 = 1) and register length L of the syndromes S_1 .. S_2t. The update
+// C <- C + (d / b) x B (b: the discrepancy of the last length change) takes one product per
+// coefficient; the inversionless form (gamma C + d x B, two products) gives the same C up to
+// a nonzero scalar at every step (by induction: its C, B and gamma are this form's times
+// the same running product of discrepancies), so the same L, degree and roots.
 template <int M, int TMAX>
 __device__ __forceinline__ void bm_locator(const uint8_t *__restrict__ ex,
                                            const uint16_t *__restrict__ lg, const uint32_t *Sw,
@@ -148,11 +180,11 @@ __device__ __forceinline__ void bm_locator(const uint8_t *__restrict__ ex,
         sq = sq >= N ? sq - N : sq;
         lS[e - 1] = (h == ZL) ? ZL : sq;
     }
-    // inversionless binary Berlekamp-Massey over S_1, S_3, ... (even steps vanish)
+    // binary Berlekamp-Massey over S_1, S_3, ... (even steps vanish)
     int lB[TMAX + 1];
 #pragma unroll
     for (int i = 0; i <= TMAX; ++i) { C[i] = i ? 0u : 1u; lB[i] = i ? ZL : 0; }
-    int lgam = 0, L = 0;
+    int lb = 0, L = 0;
 #pragma unroll
     for (int k = 0; k < TMAX; ++k) {
         if (k < t) {
@@ -168,11 +200,13 @@ __device__ __forceinline__ void bm_locator(const uint8_t *__restrict__ ex,
                 d ^= gf_exp2<M>(ex, lC[i], lS[r - i]);
             const int ld = lg[d];
             const bool chg = (d != 0u) && (2 * L <= r);
+            int lf = ld - lb;  // log(d / b); d = 0 leaves C as it is
+            lf = lf < 0 ? lf + N : lf;
+            lf = d ? lf : ZL;
 #pragma unroll
-            for (int i = TMAX; i >= 0; --i) {
+            for (int i = TMAX; i >= 1; --i) {
                 if (i > 2 * k + 1) { C[i] = 0u; continue; }
-                const uint32_t g = gf_exp2<M>(ex, lgam, lC[i]);
-                C[i] = i ? (g ^ gf_exp2<M>(ex, ld, lB[i - 1])) : g;
+                C[i] ^= gf_exp2<M>(ex, lf, lB[i - 1]);
             }
             // B <- C_old (length change) or x*B; then x*B for the skipped odd step
 #pragma unroll
@@ -185,7 +219,7 @@ __device__ __forceinline__ void bm_locator(const uint8_t *__restrict__ ex,
             for (int i = TMAX; i >= 1; --i) lB[i] = lB[i - 1];
             lB[0] = ZL;
             L = chg ? r + 1 - L : L;
-            lgam = chg ? ld : lgam;
+            lb = chg ? ld : lb;
         }
     }
     Lout = L;
@@ -582,8 +616,8 @@ __device__ __forceinline__ bool alg_decode_word(const uint8_t *ex, const uint16_
 // lane's decode costs ~(t + 1)(n + 4t) table lookups and the LDS pipe, shared by the CU's
 // four SIMDs, is the bottleneck:
 //   * Berlekamp-Massey with lane i holding coefficient i of C (and B): per step one log
-//     lookup, one product per lane for the discrepancy -- summed by M ballot parities, no
-//     LDS -- and two products per lane for the update; the exact recurrence of bm_locator.
+//     lookup, one product per lane for the discrepancy -- summed by a DPP/permlane XOR --
+//     and one product per lane for the update; the recurrence of bm_locator.
 //   * the Chien search of Decoder::locatorsAndRoots (:279-296) spread over the lanes: lane
 //     l tests the points of positions p = l + 64 s (root alpha^k flips position
 //     (n - k) mod n, :287), the locator's logs broadcast from lanes 0..deg.
@@ -619,25 +653,36 @@ __device__ __forceinline__ bool alg_decode_wave(const uint8_t *__restrict__ ex,
     uint32_t C = lane == 0 ? 1u : 0u;  // coefficient `lane` of C
     int lB = lane == 0 ? 0 : ZL;       // log of coefficient `lane` of B
     int lgam = 0, L = 0;
+    // lane i holds log S_{r - i + 1} at step k (r = 2k): two lanes further up per step, the
+    // two new syndromes entering at lanes 0 and 1. Lane moves by DPP wave shifts and the
+    // discrepancy by a DPP/permlane XOR over the wave -- no LDS crossbar (ds_bpermute) on the
+    // step's dependency chain.
+    int lsv = lane == 0 ? (int)rdl((uint32_t)lSq, 0) : ZL;
     for (int k = 0; k < t; ++k) {
         const int r = 2 * k;
         const int lC = lg[C];
         const int top = 2 * k - 1 > 0 ? (2 * k - 1 < TMAX ? 2 * k - 1 : TMAX) : 0;
-        const int lsv = __shfl(lSq, (r - lane) & 63, 64);  // log S_{r - lane + 1}
         const uint32_t term = lane <= top ? gf_exp2<M>(ex, lC, lsv) : 0u;
-        const uint32_t d = uni((int)wave_xor_bits<M>(term));
+        const uint32_t d = uni((int)wave_xor(term));
         const int ld = lg[d];
         const bool chg = (d != 0u) && (2 * L <= r);
-        const int lBm1 = __shfl(lB, (lane - 1) & 63, 64);  // B_{lane-1}
-        const int lBm2 = __shfl(lB, (lane - 2) & 63, 64);
-        const int lCm1 = __shfl(lC, (lane - 1) & 63, 64);
-        const uint32_t g = gf_exp2<M>(ex, lgam, lC);
-        const uint32_t Cn = lane ? (g ^ gf_exp2<M>(ex, ld, lBm1)) : g;
+        const int lBm1 = wave_shr1(lB, ZL);  // B_{lane-1}
+        const int lBm2 = wave_shr1(lBm1, ZL);
+        const int lCm1 = wave_shr1(lC, ZL);
+        int lf = ld - lgam;  // log(d / b), bm_locator's update with division
+        lf = lf < 0 ? lf + N : lf;
+        lf = d ? lf : ZL;
+        const uint32_t Cn = lane ? (C ^ gf_exp2<M>(ex, lf, lBm1)) : C;
         C = (lane > 2 * k + 1 || lane > TMAX) ? 0u : Cn;
         // B <- C_old (length change) or x B, then x B for the vanishing odd step
         lB = lane == 0 ? ZL : (chg ? lCm1 : (lane >= 2 ? lBm2 : ZL));
         L = chg ? r + 1 - L : L;
         lgam = chg ? ld : lgam;
+        if (k + 1 < t) {
+            const int s2 = wave_shr1(wave_shr1(lsv, ZL), ZL);
+            const int n0 = (int)rdl((uint32_t)lSq, (r + 2) & 63), n1 = (int)rdl((uint32_t)lSq, (r + 1) & 63);
+            lsv = lane == 0 ? n0 : (lane == 1 ? n1 : s2);
+        }
     }
     const uint64_t nz = ballot(C != 0u && lane <= TMAX) & ~1ull;
     const int deg = nz ? 63 - (int)__builtin_clzll(nz) : 0;

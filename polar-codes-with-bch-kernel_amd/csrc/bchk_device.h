@@ -19,7 +19,8 @@ constexpr uint32_t kFaultHeavySlot = 1u, kFaultHeavyWait = 2u, kFaultTailSlot = 
 
 // Per-code lookup tables, one device blob, copied into LDS by every workgroup.
 //   exp8 [2n]        alpha^i for i < 2n-1, exp8[2n-1] = 0 (log sums are clamped to
-//                    2n-1 = log(0), bchk_core.h gf_exp2)
+//                    2n-1 = log(0), bchk_core.h gf_exp2); m >= 7: [4n], zero from 2n-1 on
+//                    (any sum of two logs in [0, n) or 2n-1 indexes it, no clamp)
 //   log16[2^m]       log_alpha(v); log16[0] = 2n-1
 //   col  [n][W]      odd-syndrome column of position p: byte j of word j/4 =
 //                    alpha^((2j+1) p mod n), j < t   (Decoder::alterSyndromPoly :210-230)

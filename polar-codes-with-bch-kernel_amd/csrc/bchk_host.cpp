@@ -123,7 +123,7 @@ std::vector<uint8_t> make_tables(const Field &f, int t, TableDesc *td, int tmax 
     auto align16 = [](size_t v) { return (v + 15) & ~size_t(15); };
     size_t off = 0;
     td->off_exp = (uint32_t)off;
-    off = align16(off + 2 * n);
+    off = align16(off + (m >= 7 ? 4 : 2) * size_t(n));  // m >= 7: zeros past 2n-1 (gf_exp2)
     td->off_log = (uint32_t)off;
     off = align16(off + 2 * (size_t(1) << m));
     td->off_col = (uint32_t)off;

@@ -287,6 +287,99 @@ __device__ __forceinline__ void prep_syndromes(const uint32_t *col, int lane, Pr
     }
 }
 
+// Long codes, first kernel: what the first test patterns read of the order is the least
+// reliable ranks -- patterns 0..3 flip ranks 0 and 1, calcRightSide takes at most 2t + 1
+// agreeing ranks past at most t + 2 disagreeing ones, and the calcT scan decides small T
+// from ranks <= t + 2 (accept_success bails out to the search kernel past the selection).
+// So instead of sorting all n reliabilities (a 256-key bitonic network, ~1 100 VALU per
+// codeword) the kernel selects the KSEL <= 64 smallest: a binary search over the high word of
+// the |alpha| bits for a bound that between KSEL and 64 keys lie at or below (wave-uniform,
+// ballot counts), then those keys -- one per lane -- are sorted by the 64-lane network.
+template <int M, int TMAX>
+constexpr int first_ksel() { return 3 * TMAX + 4 < 31 ? 31 : 3 * TMAX + 4; }
+template <int M, int TMAX>
+constexpr bool first_sel_capable() { return Geo<M>::NW > 1 && first_ksel<M, TMAX>() <= 64; }
+
+// prep_loaded's state with ranks 0 .. nsel-1 exact (lane = rank, s = 0); false (nothing
+// decided) when no such bound exists or two selected keys share their 55-bit prefix -- the
+// caller then takes prep_loaded, whose exact rank resolves ties.
+template <int M, int TMAX>
+__device__ __forceinline__ bool prep_select(const SearchParams &p, const uint32_t *col, double *as,
+                                            double *ap, uint8_t *ordl, const double (&yv)[Geo<M>::NW],
+                                            int lane, Prep<M, TMAX> &P, int &nsel) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW, KLO = first_ksel<M, TMAX>();
+    uint32_t kh[NW];
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {  // :336-342
+        const int pos = lane + 64 * s;
+        const bool valid = pos < N;
+        const double al = (2.0 * yv[s]) / p.s2;
+        P.av[s] = valid ? fabs(al) : 0.0;
+        P.yH.w[s] = ballot(valid && !(al <= 0.0));
+        if (valid) ap[pos] = P.av[s];
+        kh[s] = valid ? (uint32_t)((uint64_t)__double_as_longlong(P.av[s]) >> 32) : 0xFFFFFFFFu;
+    }
+    auto count = [&](uint32_t h) {
+        int c = 0;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) c += __popcll(ballot(kh[s] <= h));
+        return c;
+    };
+    uint32_t h = 0x7FF00000u;  // +inf: every finite |alpha| lies at or below
+    int c = count(h);
+    if (c < KLO) return false;  // NaN samples
+    // invariant: fewer than KLO keys below lo, at least KLO at or below h
+    for (uint32_t lo = 0; c > 64 && lo < h;) {
+        const uint32_t mid = lo + ((h - lo) >> 1);
+        const int cm = count(mid);
+        if (cm >= KLO) {
+            h = mid;
+            c = cm;
+        } else {
+            lo = mid + 1;
+        }
+    }
+    if (c > 64) return false;
+    // the selected keys, one per lane, then the 64-lane network
+    double *scratch = as;  // the sorted ranks are written there after the exchange
+    int base = 0;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const bool sel = kh[s] <= h;
+        const uint64_t bal = ballot(sel);
+        const int r = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (sel)
+            scratch[r] = __longlong_as_double(
+                (long long)(((uint64_t)__double_as_longlong(P.av[s]) & ~0xFFull) | (uint64_t)(lane + 64 * s)));
+        base += __popcll(bal);
+    }
+    wave_sync();
+    uint64_t key[1];
+    key[0] = lane < c ? (uint64_t)__double_as_longlong(scratch[lane]) : ~0ull;
+    wave_sync();
+    wave_bitonic_sort<1>(key, lane);
+    const uint64_t nx = shfl64(key[0], (lane + 1) & 63);
+    if (ballot(lane + 1 < c && (key[0] >> 8) == (nx >> 8))) return false;  // a prefix tie
+    const int pos = (int)(key[0] & 0xFFull);
+    P.ordv[0] = lane < c ? pos : 0;
+    P.asv[0] = lane < c ? ap[pos] : 0.0;
+#pragma unroll
+    for (int s = 1; s < NW; ++s) {
+        P.ordv[s] = 0;
+        P.asv[s] = 0.0;
+    }
+    if (lane < c) {
+        as[lane] = P.asv[0];
+        ordl[lane] = (uint8_t)pos;
+    }
+    P.tie = false;
+    wave_sync();
+    prep_syndromes<M, TMAX>(col, lane, P);
+    nsel = c;
+    return true;
+}
+
 // The best codeword so far as a skip key: bit 63 valid, bits 32..39 u = its differences
 // from the hard decision outside the NB <= 31 least reliable positions, bits 0..30 dR = its
 // differences on them (bit b: sorted position b, the bit test pattern i flips, :36-51).
@@ -442,10 +535,15 @@ __device__ __forceinline__ void init_state(SearchState<Geo<M>::NW> &S, int varia
 // One successful decode at test pattern ii, in pattern order: the body of the reference
 // loop after `success` (:372-398). Wave-uniform inputs; the calcT scan is lane-parallel.
 // Sets S.done when the reference loop would end after this iteration.
+// Long-code first kernel (prep_select): only ranks 0 .. nsel-1 of the order are known (lane
+// = rank, s = 0). Where calcRightSide or the calcT scan would need a rank beyond them,
+// *bail is set and nothing else is decided: the codeword goes to the search kernel, which
+// starts it from scratch with the full order.
 template <int M, int TMAX>
 __device__ __forceinline__ void accept_success(SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
                                const Mask<Geo<M>::NW> &d, int m, double l, uint64_t ii,
-                               const double *as, const SearchParams &p, int lane) {
+                               const double *as, const SearchParams &p, int lane,
+                               int nsel = Geo<M>::N, bool *bail = nullptr) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
     const int t = p.t;
     if (ii == 0 || !S.firstOK) S.m0 = m; // :374 (m = calcM, l = calcL of this candidate)
@@ -457,6 +555,30 @@ __device__ __forceinline__ void accept_success(SearchState<Geo<M>::NW> &S, const
     // both are prefixes of the same sequential sum.
     const int border = (2 * t + 1) - (m + S.m0) / 2;
     const int border2 = t - (m + S.m0) / 2;
+    if (nsel < N) {
+        // selected ranks (lane = rank): the return is certain when l lies below the
+        // border-term sum formed in any order by more than its rounding (the terms are
+        // positive: the two sums differ by < 2^-47 relative at border <= 64)
+        const int op = P.ordv[0];
+        uint64_t dw = 0;
+#pragma unroll
+        for (int u = 0; u < NW; ++u) dw = (u == (op >> 6)) ? d.w[u] : dw;
+        const bool ag = lane < nsel && !((dw >> (op & 63)) & 1ull);
+        const uint64_t agm = ballot(ag);
+        if (__popcll(agm) < border) {  // needs a rank past the selection
+            *bail = true;
+            return;
+        }
+        const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(agm >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)agm, 0u));
+        const double sum = rdlf(wave_sum_f64((ag && pre < border) ? P.asv[0] : 0.0), 0);
+        if (l < sum * (1.0 - 0x1p-40)) {  // :380-382
+            S.returned = true;
+            S.i_end = ii + 1;
+            S.done = true;
+            return;
+        }
+    }
     double rs = 0.0, base2 = 0.0;
     int taken = 0;
 #pragma unroll
@@ -466,7 +588,7 @@ __device__ __forceinline__ void accept_success(SearchState<Geo<M>::NW> &S, const
         uint64_t dw = 0;
 #pragma unroll
         for (int u = 0; u < NW; ++u) dw = (u == (op >> 6)) ? d.w[u] : dw;
-        const bool ag = q < N && !((dw >> (op & 63)) & 1ull);
+        const bool ag = q < N && q < nsel && !((dw >> (op & 63)) & 1ull);
         uint64_t agm = ballot(ag);
         while (agm && taken < border) {
             const int b = (int)__builtin_ctzll(agm);
@@ -482,20 +604,26 @@ __device__ __forceinline__ void accept_success(SearchState<Geo<M>::NW> &S, const
         S.done = true;
         return;
     }
-    // calcT scan (:384): while (l >= calcT(j) && j <= n-1-t) ++j, one j per lane
+    // calcT scan (:384): while (l >= calcT(j) && j <= n-1-t) ++j, one j per lane; with a
+    // selection only j + t < nsel is known (then jstar is exact if the scan stops there)
     const int scan_last = N - 1 - t;
+    const int jlim = nsel < N ? (nsel - 1 - t < scan_last ? nsel - 1 - t : scan_last) : scan_last;
     int first = 0x7FFFFFFF;
 #pragma unroll
     for (int s = 0; s < (N + 63) / 64; ++s) {
         const int j = lane + 64 * s;
-        bool stop = true;  // j beyond the scan range stops it
-        if (j <= scan_last) {
+        bool stop = jlim == scan_last;  // j beyond the scan range stops it
+        if (j <= jlim) {
             double ct = base2;
             for (int u = 0; u <= t; ++u) ct += as[j + u];
             stop = !(l >= ct);
         }
         const uint64_t sm = ballot(stop && j < N);
         if (sm && first == 0x7FFFFFFF) first = 64 * s + (int)__builtin_ctzll(sm);
+    }
+    if (first == 0x7FFFFFFF && jlim < scan_last) {
+        *bail = true;
+        return;
     }
     const int jstar = first > scan_last + 1 ? scan_last + 1 : first;
     const bool word_variant = p.variant == BCHK_VARIANT_WORD;
@@ -538,7 +666,8 @@ __device__ __forceinline__ TxPre<Geo<M>::NW> tx_prefetch(const SearchParams &p, 
 template <int M, int TMAX>
 __device__ __forceinline__ void write_outputs(const SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
                               const SearchParams &p, uint32_t cw, int lane,
-                              TxPre<Geo<M>::NW> txp = TxPre<Geo<M>::NW>{{}, false}) {
+                              TxPre<Geo<M>::NW> txp = TxPre<Geo<M>::NW>{{}, false},
+                              unsigned long long *acc = nullptr) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
     const bool word_variant = p.variant == BCHK_VARIANT_WORD;
     const uint64_t decodes = S.i_end;
@@ -560,7 +689,14 @@ __device__ __forceinline__ void write_outputs(const SearchState<Geo<M>::NW> &S, 
             bit_errors += (uint32_t)__popcll(ballot(pos < N && x != tv));
         }
     }
-    if (p.cnt && lane == 0) {  // src/dataForPlot.cpp:55-74
+    if (p.cnt && acc) {  // the caller's per-wave sums (wave-uniform), flushed once per wave
+        acc[0] += bit_errors ? 1ull : 0ull;
+        acc[1] += (unsigned long long)bit_errors;
+        acc[2] += (unsigned long long)decodes;
+        acc[3] += (unsigned long long)(pro + iters * (uint64_t)(N + 6) + S.jsteps + S.impr);
+        acc[4] += (unsigned long long)(pro + iters * (uint64_t)(N + 1) + S.jsteps);
+        acc[5] += 1ull;
+    } else if (p.cnt && lane == 0) {  // src/dataForPlot.cpp:55-74
         unsigned long long *c = p.cnt + (size_t)(cw % (uint32_t)kCntSlots) * kCntStride;
         if (bit_errors) {
             atomicAdd(c + 0, 1ull);
@@ -602,7 +738,8 @@ template <int M, int TMAX>
 __device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
                                                const SearchParams &p, const uint8_t *ex,
                                                const uint16_t *lg, const double *as,
-                                               const double *ap, int lane) {
+                                               const double *ap, int lane,
+                                               int nsel = Geo<M>::N, bool *bail = nullptr) {
     constexpr int NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
     for (int i = 0; i < kSeqPatterns; ++i) {
         if ((uint64_t)i >= S.bound) {  // the loop ends at its bound (:361)
@@ -625,10 +762,11 @@ __device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const
 #pragma unroll
             for (int s = 0; s < NW; ++s)
                 for (uint64_t v = E.w[s]; v; v &= v - 1) l += rdlf(P.av[s], (int)__builtin_ctzll(v));
-            if (l < S.l0) accept_success<M, TMAX>(S, P, E, mask_popc<NW>(E), l, (uint64_t)i, as, p, lane);
+            if (l < S.l0)
+                accept_success<M, TMAX>(S, P, E, mask_popc<NW>(E), l, (uint64_t)i, as, p, lane, nsel, bail);
             else if (i == 0 || !S.firstOK) S.m0 = mask_popc<NW>(E);  // :374 without improvement
         }
-        if (S.done) return;
+        if (S.done || (bail && *bail)) return;
     }
 }
 
@@ -2148,7 +2286,10 @@ kaneko_search_kernel(SearchParams p) {
 // kernel, so it holds fewer registers than the search kernel and keeps more waves in flight
 // to hide the channel loads. A codeword whose search has not ended goes to the exact
 // kernel's queue (one atomic per queued codeword), which starts it from scratch.
-template <int M, int TMAX>
+// SEL (no stats record requested, so an exact tie beyond the selection is not observable):
+// the order by prep_select, and the fused counters summed per wave (one set of atomics per
+// wave instead of per codeword).
+template <int M, int TMAX, bool SEL>
 __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4)))
 kaneko_first_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2173,6 +2314,8 @@ kaneko_first_kernel(SearchParams p) {
         load_row<M>(p, cw, lane, ynext);
         txnext = tx_prefetch<M>(p, cw, lane);
     }
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+    const uint32_t cw_first = cw;
     for (; cw < p.count; cw += stride) {
         double yv[NW];
 #pragma unroll
@@ -2188,7 +2331,13 @@ kaneko_first_kernel(SearchParams p) {
         continue;
 #endif
         Prep<M, TMAX> P;
-        prep_loaded<M, TMAX>(p, col, as, ap, ordl, yv, lane, P);
+        int nsel = Geo<M>::N;
+        bool selected = false;
+        if constexpr (SEL) selected = prep_select<M, TMAX>(p, col, as, ap, ordl, yv, lane, P, nsel);
+        if (!selected) {
+            nsel = Geo<M>::N;
+            prep_loaded<M, TMAX>(p, col, as, ap, ordl, yv, lane, P);
+        }
 #if defined(BCHK_FIRST_CUT) && BCHK_FIRST_CUT == 2
         ap[lane] = P.asv[0] + (double)P.S0[0] + (double)P.Lo[0];  // + prep (sort, syndromes)
         continue;
@@ -2203,12 +2352,19 @@ kaneko_first_kernel(SearchParams p) {
 #endif
         SearchState<NW> S;
         init_state<M>(S, p.variant);
-        first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
-        if (S.done) {
-            write_outputs<M, TMAX>(S, P, p, cw, lane, txp);
+        bool bail = false;
+        first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane, nsel, &bail);
+        if (S.done && !bail) {
+            write_outputs<M, TMAX>(S, P, p, cw, lane, txp, SEL ? acc : nullptr);
         } else if (lane == 0) {
             p.queue_out[atomicAdd(p.qtail, 1u)] = cw;
         }
+    }
+    if (SEL && p.cnt && cw_first < p.count && lane == 0) {
+        unsigned long long *c = p.cnt + (size_t)(cw_first % (uint32_t)kCntSlots) * kCntStride;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (acc[k]) atomicAdd(c + k, acc[k]);
     }
 }
 
@@ -2228,10 +2384,25 @@ kaneko_first_kernel(SearchParams p) {
 #ifndef BCHK_COOP_SLOTS
 #define BCHK_COOP_SLOTS 48
 #endif
-constexpr int kCoopSlotsMax = 64;
+constexpr int kCoopSlotsMax = 128;
+// Long codes (m >= 7): a decoder wave claims kLongClaim chunks at once and decodes only
+// their patterns that can still matter -- the ones skip_lane does not rule out -- packed 64
+// to a round (lane i no longer decodes pattern base + i). At 5 dB on BCH(255,139,31) the
+// skip rules out 46 % of a heavy codeword's patterns but whole 64-pattern chunks rarely
+// (6 %: scripts/proto_m8_skip.c), so without packing most of that stayed lanes doing
+// nothing. Successes are rare (almost every pattern of a heavy codeword fails), so a ring
+// slot holds only the chunk's success mask and up to kLongRec candidate records. A chunk
+// with more candidates is decoded again, on the acceptor's request (when it reaches that
+// chunk), by a decoder wave into the one dense result buffer. A claim that lies past the
+// published loop bound waits -- the bound may rise again -- until the codeword is done or
+// the bound passes it.
+constexpr int kLongClaim = 8;
+constexpr int kLongSlots = 128;
+constexpr int kLongRec = 2;
 template <int NW>
-constexpr int coop_slots() { return NW == 1 ? BCHK_COOP_SLOTS : 16; }
-static_assert(BCHK_COOP_SLOTS <= kCoopSlotsMax, "ring flags are polled one slot per lane");
+constexpr int coop_slots() { return NW == 1 ? BCHK_COOP_SLOTS : kLongSlots; }
+static_assert(BCHK_COOP_SLOTS <= 64, "ring flags are polled one slot per lane");
+static_assert(kLongSlots <= kCoopSlotsMax && kLongSlots >= 15 * kLongClaim + 8, "every decoder's claim fits");
 
 template <int NW>
 struct CoopSlot {  // one decoded chunk
@@ -2240,6 +2411,32 @@ struct CoopSlot {  // one decoded chunk
     double l[64];
     uint32_t m[64];
 };
+template <int NW>
+struct LongRec {  // a candidate (m >= 7): pattern base + lane
+    uint64_t diff[NW];
+    double l;
+    uint32_t m, lane;
+};
+template <int NW>
+struct LongSlot {
+    uint64_t okm;    // successes (lanes = patterns of the chunk)
+    uint32_t ncand;  // candidates found; > kLongRec: only the first kLongRec stored
+    uint32_t pad;
+    double run;      // the decoder's running minimum of l (candidates lie below it)
+    LongRec<NW> rec[kLongRec];
+};
+template <int NW>
+struct LongDense {  // one chunk decoded for the acceptor: every lane's result
+    uint64_t okm;
+    uint64_t diff[64 * NW];
+    double l[64];
+    uint32_t m[64];
+};
+template <int NW>
+constexpr size_t coop_ring_bytes() {
+    return NW == 1 ? sizeof(CoopSlot<NW>) * coop_slots<NW>()
+                   : sizeof(LongSlot<NW>) * kLongSlots + ((sizeof(LongDense<NW>) + 15) & ~size_t(15));
+}
 
 struct CoopCtl {
     uint32_t next;      // next chunk to hand out
@@ -2250,6 +2447,8 @@ struct CoopCtl {
     uint64_t bound;     // the acceptor's current loop bound (diagnostics; may rise again)
     double l0;          // current l0 (monotone non-increasing)
     uint64_t skey;      // skip_key of the best codeword so far (0: none yet)
+    uint32_t redo;      // m >= 7: chunk + 1 the acceptor wants decoded densely (0: none)
+    uint32_t redo_done; // chunk + 1 whose results the dense buffer holds
     uint32_t ready[kCoopSlotsMax];  // chunk index + 1 once the slot holds that chunk
 };
 
@@ -2299,6 +2498,184 @@ __device__ uint32_t next_heavy(const SearchParams &p) {
     return kEmptySlot;
 }
 
+// k-th set bit (k from 0, k < popc(mk)) of mk, per lane, branch-free
+__device__ __forceinline__ int select_bit(uint64_t mk, int k) {
+    const uint32_t lo = (uint32_t)mk;
+    int c = __popc(lo);
+    const bool up = k >= c;
+    k = up ? k - c : k;
+    uint32_t v = up ? (uint32_t)(mk >> 32) : lo;
+    int pos = up ? 32 : 0;
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        const uint32_t low = v & ((1u << w) - 1u);
+        c = __popc(low);
+        const bool u2 = k >= c;
+        k = u2 ? k - c : k;
+        v = u2 ? (v >> w) : low;
+        pos += u2 ? w : 0;
+    }
+    return pos;
+}
+
+template <int NW>
+__device__ __forceinline__ void mask_flip(Mask<NW> &m, int p) {
+#pragma unroll
+    for (int s = 0; s < NW; ++s) m.w[s] ^= (uint64_t)((p >> 6) == s) << (p & 63);
+}
+
+// A decoder wave's claim of kLongClaim chunks c .. c + 7 (m >= 7; c a multiple of 8): the
+// patterns skip_lane leaves, packed 64 per round (the k-th of them in lane k), decoded; each
+// success goes, in pattern order, into its chunk's success mask and -- when it is a strict
+// running minimum of l below l0 as published (the candidates of the dense ring) -- into the
+// chunk's slot. Chunks at or past the published bound are marked, not decoded; chunks past
+// the cap are not published.
+template <int M, int TMAX>
+__device__ __forceinline__ void long_decode_claim(const Prep<M, TMAX> &P, uint32_t c, uint64_t capc, uint64_t bnd,
+                                                  double l0r, uint64_t skey, int t, const uint8_t *ex,
+                                                  const uint16_t *lg, const uint64_t *chien, const double *ap,
+                                                  void *wscratch, LongSlot<Geo<M>::NW> *ring, CoopCtl *ctl,
+                                                  int lane) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W, G = kLongClaim;
+    constexpr int NB = N < 31 ? N : 31;
+    static_assert(G == 8, "pattern bits 6..8 select the chunk within a claim");
+    // per-wave LDS scratch (the wave's sorted-|alpha| slice, used by the acceptor only):
+    // the chunks' pattern masks and the syndromes of the hard decision ^ pattern bits >= 6
+    uint64_t *actl = reinterpret_cast<uint64_t *>(wscratch);
+    uint32_t *hl = reinterpret_cast<uint32_t *>(actl + G);
+    int pre[G + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint64_t b = 64ull * (uint64_t)(c + (uint32_t)g);
+        const uint64_t a = (b < capc && b < bnd) ? ballot(!skip_lane(skey, b + (uint64_t)lane, t)) : 0ull;
+        if (lane == 0) actl[g] = a;
+        pre[g + 1] = pre[g] + __popcll(a);
+        if (b < capc && lane == 0) {  // the slot's running state (the ring space is ours)
+            LongSlot<NW> &S = ring[(c + (uint32_t)g) % kLongSlots];
+            S.okm = 0ull;
+            S.ncand = 0u;
+            S.run = l0r;
+        }
+    }
+    {   // lane g < 8: the syndrome of pattern bits >= 6 for chunk c + g
+        uint32_t h[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) h[w] = P.S0[w];
+        const uint32_t hb = (c + (uint32_t)(lane & 7)) << 6;
+        for (int b = 6; b < NB; ++b) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t col_b = rdl(P.scol[w], b);
+                h[w] ^= ((hb >> b) & 1u) ? col_b : 0u;
+            }
+        }
+        if (lane < G) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) hl[lane * W + w] = h[w];
+        }
+    }
+    wave_sync();
+    const int A = pre[G];
+    for (int r = 0; 64 * r < A; ++r) {
+        const int idx = 64 * r + lane;
+        const bool valid = idx < A;
+        int g = 0, pg = 0;
+#pragma unroll
+        for (int gg = 1; gg < G; ++gg) {
+            g = idx >= pre[gg] ? gg : g;
+            pg = idx >= pre[gg] ? pre[gg] : pg;
+        }
+        const int bit = valid ? select_bit(actl[g], idx - pg) : 0;
+        uint32_t Sw[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) Sw[w] = hl[g * W + w] ^ (uint32_t)__shfl((int)P.Lo[w], bit, 64);
+        Mask<NW> E;
+        const bool ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, t, E, valid) && valid;
+        const uint64_t okb = ballot(ok);
+        if (!okb) continue;
+        // the successes (rare): diff = flipped positions ^ error locations, m, calcL (:69-77)
+        const uint32_t ii = 64u * (c + (uint32_t)g) + (uint32_t)bit;
+        Mask<NW> d = E;
+        double l = 0.0;
+        int m = 0;
+        if (ok) {
+            for (int b = 0; b < NB; ++b) {
+                const int pb = (int)rdl((uint32_t)P.ordb, b);
+                if ((ii >> b) & 1u) mask_flip<NW>(d, pb);
+            }
+            m = mask_popc<NW>(d);
+#pragma unroll
+            for (int s2 = 0; s2 < NW; ++s2)
+                for (uint64_t v = d.w[s2]; v; v &= v - 1) l += ap[64 * s2 + (int)__builtin_ctzll(v)];
+        }
+        for (uint64_t sm = okb; sm; sm &= sm - 1) {  // pattern order (lane order in a round)
+            const int L = (int)__builtin_ctzll(sm);
+            const int gL = (int)rdl((uint32_t)g, L), bL = (int)rdl((uint32_t)bit, L);
+            const double lL = rdlf(l, L);
+            LongSlot<NW> &S = ring[(c + (uint32_t)gL) % kLongSlots];
+            const bool cand = lL < S.run;
+            const uint32_t slot_n = S.ncand;
+            wave_sync();
+            if (lane == 0) {
+                S.okm |= 1ull << bL;
+                if (cand) {
+                    S.run = lL;
+                    S.ncand = slot_n + 1u;
+                }
+            }
+            if (cand && slot_n < (uint32_t)kLongRec && lane == L) {
+                LongRec<NW> &R = S.rec[slot_n];
+#pragma unroll
+                for (int s2 = 0; s2 < NW; ++s2) R.diff[s2] = d.w[s2];
+                R.l = l;
+                R.m = (uint32_t)m;
+                R.lane = (uint32_t)bL;
+            }
+            wave_sync();
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint32_t cg = c + (uint32_t)g;
+        if (64ull * cg >= capc) break;  // never read by the acceptor
+        if (lane == 0) lds_st(&ctl->ready[cg % kLongSlots], cg + 1u);
+    }
+    wave_sync();
+}
+
+// A decoder wave serves a pending dense request (the acceptor's, for an overflowing chunk):
+// every lane's result of the chunk into the dense buffer. true if it served one.
+template <int M, int TMAX>
+__device__ __forceinline__ bool long_serve_redo(const Prep<M, TMAX> &P, const SearchParams &p, CoopCtl *ctl,
+                                                LongDense<Geo<M>::NW> *dn, const uint8_t *ex,
+                                                const uint16_t *lg, const uint64_t *chien, const double *ap,
+                                                int lane) {
+    constexpr int NW = Geo<M>::NW;
+    uint32_t r = 0;
+    if (lane == 0) {
+        r = lds_ld(&ctl->redo);
+        if (r && atomicCAS(&ctl->redo, r, 0u) != r) r = 0;
+    }
+    r = (uint32_t)__shfl((int)r, 0, 64);
+    if (!r) return false;
+    Mask<NW> dd[1];
+    int mm[1];
+    double ll[1];
+    bool okk[1];
+    decode_chunks<M, TMAX, 1, false>(P, 64ull * (r - 1u), p.t, ex, lg, chien, ap, p.tab, dd, mm, ll, okk, 0ull);
+#pragma unroll
+    for (int s2 = 0; s2 < NW; ++s2) dn->diff[lane * NW + s2] = dd[0].w[s2];
+    dn->l[lane] = ll[0];
+    dn->m[lane] = (uint32_t)mm[0];
+    const uint64_t okm = ballot(okk[0]);
+    if (lane == 0) dn->okm = okm;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) lds_st(&ctl->redo_done, r);
+    return true;
+}
+
 template <int M, int TMAX, bool TAB>
 __global__ void __launch_bounds__(kWaveSize * kCoopWaves)
 kaneko_coop_kernel(SearchParams p) {
@@ -2326,8 +2703,10 @@ kaneko_coop_kernel(SearchParams p) {
     const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint8_t *shared0 = smem + ((p.td.bytes + 15) & ~15u);
-    CoopSlot<NW> *ring = reinterpret_cast<CoopSlot<NW> *>(shared0);
-    CoopCtl *ctl = reinterpret_cast<CoopCtl *>(ring + kCoopSlots);
+    CoopSlot<NW> *ring = reinterpret_cast<CoopSlot<NW> *>(shared0);    // n <= 63
+    LongSlot<NW> *lring = reinterpret_cast<LongSlot<NW> *>(shared0);   // m >= 7
+    LongDense<NW> *ldense = reinterpret_cast<LongDense<NW> *>(shared0 + sizeof(LongSlot<NW>) * kLongSlots);
+    CoopCtl *ctl = reinterpret_cast<CoopCtl *>(shared0 + coop_ring_bytes<NW>());
     uint8_t *wbase = reinterpret_cast<uint8_t *>(ctl + 1) + wid * Smem<M, TMAX>::WAVE_BYTES;
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
@@ -2343,6 +2722,8 @@ kaneko_coop_kernel(SearchParams p) {
             ctl->next = 0;
             ctl->consumed = 0;
             ctl->done = 0;
+            ctl->redo = 0;
+            ctl->redo_done = 0;
         }
         if (threadIdx.x < kCoopSlots) ctl->ready[threadIdx.x] = 0;
         __syncthreads();
@@ -2373,7 +2754,48 @@ kaneko_coop_kernel(SearchParams p) {
         unsigned long long t_prev = __builtin_amdgcn_s_memtime();
         dg[0] = t_prev - t_start;
 #endif
-        if (wid != kAcceptor) {
+        if (NW > 1 && wid != kAcceptor) {
+            // ------------------------------------------------ decoder, m >= 7 (packed)
+            for (bool fin = false; !fin;) {
+                uint32_t c = 0;
+                if (lane == 0) c = atomicAdd(&ctl->next, (uint32_t)kLongClaim);
+                c = (uint32_t)__shfl((int)c, 0, 64);
+                // wait for ring space, and while the claim lies past the published bound (it
+                // may rise again) or the cap: the codeword's end (done) releases the wave;
+                // dense requests are served meanwhile
+                for (uint32_t spins = 0;; ++spins) {
+                    if (lds_ld(&ctl->done)) { fin = true; break; }
+                    if constexpr (NW > 1)
+                        if (long_serve_redo<M, TMAX>(P, p, ctl, ldense, ex, lg, chien, ap, lane)) spins = 0;
+                    const uint64_t b0 = 64ull * c;
+                    if (c + (uint32_t)(kLongClaim - 1) < lds_ld(&ctl->consumed) + kLongSlots &&
+                        b0 < lds_ld64(&ctl->bound) && b0 < capc)
+                        break;
+                    if (spins > kSpinLimit) {
+#ifdef BCHK_COOP_DEBUG
+                        if (lane == 0)
+                            printf("dec wid %d cw %u claim %u consumed %u bound %llu done %u redo %u/%u next %u\n", wid, cw, c,
+                                   lds_ld(&ctl->consumed), (unsigned long long)lds_ld64(&ctl->bound),
+                                   lds_ld(&ctl->done), lds_ld(&ctl->redo), lds_ld(&ctl->redo_done), lds_ld(&ctl->next));
+#endif
+                        flag_fault(p, kFaultCoopRing);
+                        fin = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (fin) break;
+                const double l0r = __longlong_as_double((long long)lds_ld64(
+                    reinterpret_cast<const uint64_t *>(&ctl->l0)));
+                const uint64_t skey = lds_ld64(&ctl->skey);  // a codeword found before chunk c
+                if constexpr (NW > 1)
+                    long_decode_claim<M, TMAX>(P, c, capc, ~0ull, l0r, skey, p.t, ex, lg, chien, ap, as, lring, ctl,
+                                               lane);
+#ifdef BCHK_DIAG
+                dg[3] += kLongClaim;
+#endif
+            }
+        } else if (wid != kAcceptor) {
             // ------------------------------------------------------------ decoder
             constexpr int G = chunk_group<TAB>();
             for (;;) {
@@ -2466,9 +2888,17 @@ kaneko_coop_kernel(SearchParams p) {
                 const uint32_t cj = c + (uint32_t)lane;
                 const bool rdy = lane < kCoopSlots && lds_ld(&ctl->ready[cj % kCoopSlots]) == cj + 1u;
                 const uint64_t rm = ballot(rdy);
-                const int run = (int)__builtin_ctzll(~rm);  // chunks c .. c + run - 1 ready
+                // chunks c .. c + run - 1 ready (all 64 polled: the long-code ring has 128
+                // slots, and ctz of 0 is undefined -- -1 on gfx950)
+                const int run = ~rm ? (int)__builtin_ctzll(~rm) : 64;
                 if (run == 0) {
                     if (++spins > kSpinLimit) {  // never expected: fail the codeword, no hang
+#ifdef BCHK_COOP_DEBUG
+                        if (lane == 0)
+                            printf("acc cw %u c %u bound %llu next %u ready[c] %u l0 %g redo %u/%u\n", cw, c,
+                                   (unsigned long long)S.bound, lds_ld(&ctl->next), lds_ld(&ctl->ready[c % kCoopSlots]),
+                                   S.l0, lds_ld(&ctl->redo), lds_ld(&ctl->redo_done));
+#endif
                         if (lane == 0) flag_fault(p, kFaultCoopRing);
                         S.i_end = 64ull * c;
                         S.truncated = true;
@@ -2483,9 +2913,72 @@ kaneko_coop_kernel(SearchParams p) {
                 dg[1] += t_a - t_w;
                 const uint64_t impr0 = S.impr;
 #endif
-                const uint64_t candj = lane < run ? ring[cj % kCoopSlots].cand : 0ull;
-                if (c == 0 && !(ring[0].okm & 1ull)) S.firstOK = false;  // :371
                 uint32_t cdone = c + (uint32_t)run;
+                if constexpr (NW > 1) {
+                    // m >= 7: the candidate records, or the chunk decoded here (marked past
+                    // the bound, or more candidates than the slot holds)
+                    const bool need = lane < run && lring[cj % kLongSlots].ncand != 0u;
+                    if (c == 0 && !(lring[0].okm & 1ull)) S.firstOK = false;  // :371
+                    for (uint64_t jm = ballot(need); jm; jm &= jm - 1) {
+                        const int j = (int)__builtin_ctzll(jm);
+                        const uint32_t cc = c + (uint32_t)j;
+                        const uint64_t base = 64ull * cc;
+                        if (base >= S.bound || base >= capc) { cdone = cc; break; }
+                        const LongSlot<NW> &sl = lring[cc % kLongSlots];
+                        if (sl.ncand > (uint32_t)kLongRec) {
+                            // more candidates than the slot holds: a decoder wave decodes the
+                            // chunk densely for us (all earlier chunks are consumed, so no
+                            // decoder is waiting on us for it)
+                            if (lane == 0) lds_st(&ctl->redo, cc + 1u);
+                            uint32_t sp = 0;
+                            while (lds_ld(&ctl->redo_done) != cc + 1u && ++sp < kSpinLimit) __builtin_amdgcn_s_sleep(1);
+                            if (sp >= kSpinLimit) {
+#ifdef BCHK_COOP_DEBUG
+                                if (lane == 0)
+                                    printf("acc dense wait cw %u cc %u redo %u/%u\n", cw, cc, lds_ld(&ctl->redo),
+                                           lds_ld(&ctl->redo_done));
+#endif
+                                if (lane == 0) flag_fault(p, kFaultCoopRing);
+                                S.i_end = base;
+                                S.truncated = true;
+                                S.done = true;
+                                cdone = cc;
+                                break;
+                            }
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                            for (uint64_t im = ldense->okm; im; im &= im - 1) {
+                                const int L = (int)__builtin_ctzll(im);
+                                const uint64_t ii = base + (uint64_t)L;
+                                if (ii >= S.bound) break;
+                                const double lL = ldense->l[L];
+                                if (!(lL < S.l0)) continue;
+                                Mask<NW> d;
+#pragma unroll
+                                for (int s2 = 0; s2 < NW; ++s2) d.w[s2] = ldense->diff[L * NW + s2];
+                                accept_success<M, TMAX>(S, P, d, (int)ldense->m[L], lL, ii, as, p, lane);
+                                if (S.done) break;
+                            }
+                            if (lane == 0) lds_st(&ctl->redo_done, 0u);
+                        } else {
+                            const int nc = (int)sl.ncand;
+                            for (int q = 0; q < nc; ++q) {
+                                const LongRec<NW> &R = sl.rec[q];
+                                const uint64_t ii = base + (uint64_t)R.lane;
+                                if (ii >= S.bound) break;
+                                const double lL = R.l;
+                                if (!(lL < S.l0)) continue;
+                                Mask<NW> d;
+#pragma unroll
+                                for (int s2 = 0; s2 < NW; ++s2) d.w[s2] = R.diff[s2];
+                                accept_success<M, TMAX>(S, P, d, (int)R.m, lL, ii, as, p, lane);
+                                if (S.done) break;
+                            }
+                        }
+                        if (S.done) { cdone = cc + 1u; break; }
+                    }
+                }
+                const uint64_t candj = (NW == 1 && lane < run) ? ring[cj % kCoopSlots].cand : 0ull;
+                if (NW == 1 && c == 0 && !(ring[0].okm & 1ull)) S.firstOK = false;  // :371
                 for (uint64_t jm = ballot(candj != 0ull); jm; jm &= jm - 1) {
                     const int j = (int)__builtin_ctzll(jm);
                     const uint32_t cc = c + (uint32_t)j;
@@ -2704,7 +3197,14 @@ template <int M, int TMAX>
 static hipError_t launch_first_impl(const SearchParams &p, size_t lds, hipStream_t s) {
     const uint32_t per_block = kWavesPerBlock * kFirstPerWave;
     const int blocks = (int)((p.count + per_block - 1) / per_block);
-    hipLaunchKernelGGL((kaneko_first_kernel<M, TMAX>), dim3(blocks > 0 ? blocks : 1),
+    if constexpr (first_sel_capable<M, TMAX>()) {
+        if (!p.st && !getenv("BCHK_FIRST_FULLSORT")) {
+            hipLaunchKernelGGL((kaneko_first_kernel<M, TMAX, true>), dim3(blocks > 0 ? blocks : 1),
+                               dim3(kWaveSize * kWavesPerBlock), lds, s, p);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((kaneko_first_kernel<M, TMAX, false>), dim3(blocks > 0 ? blocks : 1),
                        dim3(kWaveSize * kWavesPerBlock), lds, s, p);
     return hipGetLastError();
 }
@@ -2726,7 +3226,7 @@ bool select_first_long(int m, int t, FastFn *out) {
 template <int M, int TMAX>
 static KernelSet make_set() {
     constexpr int NW = Geo<M>::NW;
-    const size_t coop = sizeof(CoopSlot<NW>) * coop_slots<NW>() + sizeof(CoopCtl) +
+    const size_t coop = coop_ring_bytes<NW>() + sizeof(CoopCtl) +
                         (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES;
     KernelSet k{};
     k.search = &launch_search_impl<M, TMAX, false, false>;

@@ -550,3 +550,106 @@ def test_small_code_uncapped_tail_lists_codewords(m, t, J, snr):
     o = Oracle(m, t)
     r2, l2, s2, a2 = o.kaneko_batch(y[rows], J=J)
     check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, a[0][rows], a[1][rows], a[2][rows])
+
+
+@pytest.mark.parametrize("m,t", [(8, 15), (7, 10)])
+@pytest.mark.parametrize("snr,J", [(5.0, 15), (6.0, -1), (7.0, 15)])
+def test_long_code_selection_equals_full_sort(m, t, snr, J):
+    # Long codes without a stats record: kaneko_first_kernel<.., SEL = true> orders only the
+    # ~3t + 4 least reliable positions (a bound on |alpha| found by binary search, then a
+    # 64-lane sort) and bails out to the search kernel where calcRightSide / the calcT scan
+    # would read past them; with a stats record it sorts all n. Both must give the same
+    # words, l0 bits and fused counters, also on rows with exact / prefix ties inside and
+    # beyond the selection and tiny / huge samples; a sample against the oracle.
+    import torch
+    d = dec(m, t, J=J)
+    B = 1 << 14
+    tx, y, _ = d.generate(snr, B, seed=31)
+    y = y.copy()
+    n = d.n
+    rng = np.random.default_rng(7)
+    rows = rng.choice(B, 512, replace=False)
+    for k, r in enumerate(rows):
+        o = np.argsort(np.abs(y[r]))
+        if k % 4 == 0:    # exact tie among the reliable positions (beyond the selection)
+            y[r, o[-2]] = np.copysign(abs(y[r, o[-1]]), y[r, o[-2]])
+        elif k % 4 == 1:  # exact tie inside the selection (ranks 3 / 4)
+            y[r, o[4]] = -np.copysign(abs(y[r, o[3]]), y[r, o[3]])
+        elif k % 4 == 2:  # prefix tie (1 ulp) at ranks 10 / 11
+            y[r, o[11]] = np.nextafter(y[r, o[10]], np.inf if y[r, o[10]] > 0 else -np.inf)
+        else:             # tiny and huge samples
+            y[r, o[0]] = 1e-300
+            y[r, o[-1]] = -1e300
+    dy = torch.from_numpy(y).cuda()
+    dtx = torch.from_numpy(tx).cuda()
+    outs = []
+    for fused in (False, True):
+        dres = torch.zeros((B, n), dtype=torch.uint8, device="cuda")
+        dl0 = torch.zeros(B, dtype=torch.float64, device="cuda")
+        dst = torch.zeros((B, 56), dtype=torch.uint8, device="cuda")
+        c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        d.set_max_decodes(1 << 16)
+        if fused:
+            d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), 0,
+                                  c6.data_ptr())
+        else:
+            d.decode_device(dy.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), dst.data_ptr())
+            d.count_device(dtx.data_ptr(), dres.data_ptr(), dst.data_ptr(), B, c6.data_ptr())
+        d.sync()
+        d.set_max_decodes(0)
+        outs.append((dres.cpu().numpy(), dl0.cpu().numpy(), c6.cpu().numpy(), dst.cpu().numpy()))
+    (r0, l0a, c0, st0), (r1, l0b, c1, _) = outs
+    np.testing.assert_array_equal(r0, r1)
+    np.testing.assert_array_equal(l0a.view(np.uint64), l0b.view(np.uint64))
+    np.testing.assert_array_equal(c0, c1)
+    st = st0.view(load().STATS_DTYPE).reshape(B)
+    F = load()
+    keep = np.flatnonzero(((st["flags"] & (F.F_TIE | F.F_TRUNCATED)) == 0) & (st["decodes"] < 3000))
+    idx = np.concatenate([np.intersect1d(rows, keep)[:64], rng.choice(keep, 128, replace=False)])
+    r2, l2, s2, a2 = Oracle(m, t).kaneko_batch(y[idx], J=J)
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, r1[idx], l0b[idx], st[idx])
+
+
+def test_config5_bch255_batch_heavy_rows_match_exact_path_and_oracle():
+    # Config 5's per-GPU share at its hardest point: 2^17 BCH(255,139,31) words at 5 dB,
+    # J = 15, where ~3 % of the words run the Kaneko loop to its 2^15 - 1 bound in the
+    # cooperative kernel (packed long-code decoders, sparse ring). Every row of the default
+    # path (first-pattern kernel, search kernel, cooperative kernel) -- with a stats record,
+    # and through the fused call without one -- equals the exact-only path (one wave per
+    # codeword, every pattern in order); 512 of the heavy rows (more than 8 chunks of
+    # patterns, most of them at the 32 767-decode bound) and 128 others equal the oracle.
+    import torch
+    F = load()
+    d = dec(8, 15, J=15)
+    ex = dec(8, 15, J=15, path="exact-only")
+    B = 1 << 17
+    tx, y, _ = d.generate(5.0, B, seed=43)
+    a = d.decode(y)
+    b = ex.decode(y)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+    np.testing.assert_array_equal(a[2], b[2])
+    # the fused call (no stats record: the selection first kernel, per-wave counters)
+    dy, dtx = torch.from_numpy(y).cuda(), torch.from_numpy(tx).cuda()
+    dres = torch.zeros((B, d.n), dtype=torch.uint8, device="cuda")
+    dl0 = torch.zeros(B, dtype=torch.float64, device="cuda")
+    c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), 0, c6.data_ptr())
+    d.sync()
+    acc = (a[2]["flags"] & F.F_ACCEPTED) != 0
+    r1 = dres.cpu().numpy()
+    np.testing.assert_array_equal(r1[acc], a[0][acc])
+    np.testing.assert_array_equal(dl0.cpu().numpy()[acc].view(np.uint64), a[1][acc].view(np.uint64))
+    err = (np.where(acc[:, None], a[0], 0) != tx).sum(axis=1)
+    st = a[2]
+    np.testing.assert_array_equal(c6.cpu().numpy(), [int((err > 0).sum()), int(err.sum()), int(st["decodes"].sum()),
+                                                     int(st["comparisons"].sum()), int(st["sums"].sum()), B])
+    heavy = np.flatnonzero(st["decodes"] > 8 * 64)
+    assert heavy.size >= 512 and (st["decodes"][heavy] > 5000).sum() >= 256
+    rng = np.random.default_rng(11)
+    idx = np.concatenate([rng.choice(heavy, 512, replace=False),
+                          rng.choice(np.setdiff1d(np.arange(B), heavy), 128, replace=False)])
+    r2, l2, s2, a2 = Oracle(8, 15).kaneko_batch(y[idx], J=15)
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, a[0][idx], a[1][idx], st[idx])

@@ -10,10 +10,10 @@ the reference binary by tests/test_oracle.py):
 * 5 and 6 dB: every one of the 2^20 rows (word, l0 bits) and the six fused counters equal
   to the oracle's sums; the per-row counters (from the same inputs decoded with a stats
   record) equal to the oracle's on every row.
-* 4 dB (the oracle needs ~1 CPU-minute per 2^16 rows there): every row the fast path and
-  the first exact pass did not finish is known from the stats run; 512 of those (the
-  analytic-tail / cooperative rows) plus 4096 random rows go to the oracle, and the fused
-  counters equal the stats run's sums.
+* 4 dB: every row the fast path and the first exact pass did not finish (known from the
+  stats run: ~20 000 analytic-tail / cooperative rows, the oracle's threads take about a
+  minute) plus 4096 random rows go to the oracle; all 2^20 rows equal the cooperative path
+  without the analytic tail; the fused counters equal the stats run's sums.
 * Config 4's data shape on one GPU: the 2^23-word batch (the eight ranks' jump-ahead 2^20
   shards of bench.py, concatenated) decoded in ONE call gives the sum of the eight shard
   calls' counters and the same rows.
@@ -131,10 +131,27 @@ def test_bench_step_matches_oracle(snr):
     heavy = np.flatnonzero(st["decodes"] > 2 + 8 * CHUNK)  # past the first pass's chunks
     if snr >= 5.0:
         rows = np.arange(B)
-    else:
+    else:  # every heavy row (the analytic tail's and the cooperative kernel's) + 4096 others
         rng = np.random.default_rng(11)
-        rows = np.unique(np.concatenate([rng.choice(heavy, min(512, len(heavy)), replace=False),
-                                         rng.choice(B, 4096, replace=False)]))
+        rows = np.unique(np.concatenate([heavy, rng.choice(B, 4096, replace=False)]))
+        # and every row against the cooperative path without the analytic tail (hand-off
+        # to the cooperative kernel after the first chunk: test_gpu_parity.PATHS coop-heavy)
+        import os
+        old_lim = os.environ.get("BCHK_CHUNK_LIMIT")
+        os.environ["BCHK_CHUNK_LIMIT"] = "1"
+        try:
+            dc = F.KanekoKernelProcessor(M, T, J=J)
+        finally:
+            os.environ.pop("BCHK_CHUNK_LIMIT")
+            if old_lim is not None:
+                os.environ["BCHK_CHUNK_LIMIT"] = old_lim
+        dc.set_analytic(False)
+        cres, cl0, cst = stats_run(dc, dy, B)
+        np.testing.assert_array_equal(cres, res)
+        np.testing.assert_array_equal(cl0.view(np.uint64), l0.view(np.uint64))
+        np.testing.assert_array_equal(cst, st)
+        assert dc.path_counts()[1] >= len(heavy)
+        dc.close()
     r2, l2, s2, a2 = o.kaneko_batch(y[rows], J=J)
     assert_rows_equal_oracle(rows, res, l0, st, r2, l2, s2, a2)
     if snr >= 5.0:  # every row: the fused counters are the oracle's
