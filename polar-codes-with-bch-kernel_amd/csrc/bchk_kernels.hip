@@ -45,7 +45,10 @@ struct Smem {
     // sorted |alpha| (f64), |alpha| by position (f64), order (u8)
     static constexpr int WAVE_BYTES = NP * 8 * 2 + NP;
 };
-constexpr int kCoopWaves = 16;  // waves that share one heavy codeword (1024 threads)
+#ifndef BCHK_COOP_WAVES
+#define BCHK_COOP_WAVES 16
+#endif
+constexpr int kCoopWaves = BCHK_COOP_WAVES;  // waves that share one heavy codeword (1024 threads)
 // long codes: test patterns decoded one at a time by the whole wave before the 64-pattern
 // chunks (search_codeword)
 #ifndef BCHK_SEQ_PATTERNS
@@ -2402,7 +2405,8 @@ constexpr int kLongRec = 2;
 template <int NW>
 constexpr int coop_slots() { return NW == 1 ? BCHK_COOP_SLOTS : kLongSlots; }
 static_assert(BCHK_COOP_SLOTS <= 64, "ring flags are polled one slot per lane");
-static_assert(kLongSlots <= kCoopSlotsMax && kLongSlots >= 15 * kLongClaim + 8, "every decoder's claim fits");
+static_assert(kLongSlots <= kCoopSlotsMax && kLongSlots >= (kCoopWaves - 1) * kLongClaim + 8,
+              "every decoder's claim fits");
 
 template <int NW>
 struct CoopSlot {  // one decoded chunk
@@ -2447,6 +2451,7 @@ struct CoopCtl {
     uint64_t bound;     // the acceptor's current loop bound (diagnostics; may rise again)
     double l0;          // current l0 (monotone non-increasing)
     uint64_t skey;      // skip_key of the best codeword so far (0: none yet)
+    uint32_t go;        // m >= 7: the acceptor has decoded the first patterns and published
     uint32_t redo;      // m >= 7: chunk + 1 the acceptor wants decoded densely (0: none)
     uint32_t redo_done; // chunk + 1 whose results the dense buffer holds
     uint32_t ready[kCoopSlotsMax];  // chunk index + 1 once the slot holds that chunk
@@ -2531,7 +2536,7 @@ __device__ __forceinline__ void mask_flip(Mask<NW> &m, int p) {
 // chunk's slot. Chunks at or past the published bound are marked, not decoded; chunks past
 // the cap are not published.
 template <int M, int TMAX>
-__device__ __forceinline__ void long_decode_claim(const Prep<M, TMAX> &P, uint32_t c, uint64_t capc, uint64_t bnd,
+__device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_t c, uint64_t capc, uint64_t bnd,
                                                   double l0r, uint64_t skey, int t, const uint8_t *ex,
                                                   const uint16_t *lg, const uint64_t *chien, const double *ap,
                                                   void *wscratch, LongSlot<Geo<M>::NW> *ring, CoopCtl *ctl,
@@ -2643,6 +2648,7 @@ __device__ __forceinline__ void long_decode_claim(const Prep<M, TMAX> &P, uint32
         if (lane == 0) lds_st(&ctl->ready[cg % kLongSlots], cg + 1u);
     }
     wave_sync();
+    return (A + 63) >> 6;  // decode rounds
 }
 
 // A decoder wave serves a pending dense request (the acceptor's, for an overflowing chunk):
@@ -2724,6 +2730,7 @@ kaneko_coop_kernel(SearchParams p) {
             ctl->done = 0;
             ctl->redo = 0;
             ctl->redo_done = 0;
+            ctl->go = 0;
         }
         if (threadIdx.x < kCoopSlots) ctl->ready[threadIdx.x] = 0;
         __syncthreads();
@@ -2754,6 +2761,27 @@ kaneko_coop_kernel(SearchParams p) {
         unsigned long long t_prev = __builtin_amdgcn_s_memtime();
         dg[0] = t_prev - t_start;
 #endif
+        if constexpr (NW > 1) {
+            // m >= 7: the acceptor decodes the first kSeqPatterns patterns itself before the
+            // decoders start (first_patterns; chunk 0 decodes them again, none of them is an
+            // improvement a second time), so the loop bound and the skip key of the best
+            // codeword -- at 5 dB usually the hard decision's -- are known from the first
+            // claim on: otherwise the first claims (15 x 8 chunks) decode, and Chien-scan,
+            // every pattern that only re-finds that codeword
+            if (wid == kAcceptor) {
+                first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
+                const uint64_t skey0 = S.accepted ? skip_key<M, TMAX>(S.best, P, lane) : 0ull;
+                if (lane == 0) {
+                    lds_st64(&ctl->bound, S.bound);
+                    lds_st64(reinterpret_cast<uint64_t *>(&ctl->l0), (uint64_t)__double_as_longlong(S.l0));
+                    lds_st64(&ctl->skey, skey0);
+                    if (S.done) lds_st(&ctl->done, 1u);
+                    lds_st(&ctl->go, 1u);
+                }
+            } else {
+                for (uint32_t sp = 0; !lds_ld(&ctl->go) && ++sp < kSpinLimit;) __builtin_amdgcn_s_sleep(2);
+            }
+        }
         if (NW > 1 && wid != kAcceptor) {
             // ------------------------------------------------ decoder, m >= 7 (packed)
             for (bool fin = false; !fin;) {
@@ -2763,6 +2791,9 @@ kaneko_coop_kernel(SearchParams p) {
                 // wait for ring space, and while the claim lies past the published bound (it
                 // may rise again) or the cap: the codeword's end (done) releases the wave;
                 // dense requests are served meanwhile
+#ifdef BCHK_DIAG
+                const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
+#endif
                 for (uint32_t spins = 0;; ++spins) {
                     if (lds_ld(&ctl->done)) { fin = true; break; }
                     if constexpr (NW > 1)
@@ -2784,16 +2815,23 @@ kaneko_coop_kernel(SearchParams p) {
                     }
                     __builtin_amdgcn_s_sleep(2);
                 }
+#ifdef BCHK_DIAG
+                const unsigned long long tw1 = __builtin_amdgcn_s_memtime();
+                dg[5] += tw1 - tw0;  // m >= 7 decoders: cycles waiting (ring space, bound, done)
+#endif
                 if (fin) break;
                 const double l0r = __longlong_as_double((long long)lds_ld64(
                     reinterpret_cast<const uint64_t *>(&ctl->l0)));
                 const uint64_t skey = lds_ld64(&ctl->skey);  // a codeword found before chunk c
+                int rounds = 0;
                 if constexpr (NW > 1)
-                    long_decode_claim<M, TMAX>(P, c, capc, ~0ull, l0r, skey, p.t, ex, lg, chien, ap, as, lring, ctl,
-                                               lane);
+                    rounds = long_decode_claim<M, TMAX>(P, c, capc, ~0ull, l0r, skey, p.t, ex, lg, chien, ap, as, lring,
+                                                        ctl, lane);
 #ifdef BCHK_DIAG
-                dg[3] += kLongClaim;
+                dg[3] += (unsigned long long)rounds;  // m >= 7: decode rounds of 64 packed patterns
+                dg[4] += __builtin_amdgcn_s_memtime() - tw1;  // m >= 7 decoders: cycles in claims
 #endif
+                (void)rounds;
             }
         } else if (wid != kAcceptor) {
             // ------------------------------------------------------------ decoder
@@ -2917,8 +2955,8 @@ kaneko_coop_kernel(SearchParams p) {
                 if constexpr (NW > 1) {
                     // m >= 7: the candidate records, or the chunk decoded here (marked past
                     // the bound, or more candidates than the slot holds)
+                    // (firstOK, :371, was decided by first_patterns: pattern 0 may be skipped here)
                     const bool need = lane < run && lring[cj % kLongSlots].ncand != 0u;
-                    if (c == 0 && !(lring[0].okm & 1ull)) S.firstOK = false;  // :371
                     for (uint64_t jm = ballot(need); jm; jm &= jm - 1) {
                         const int j = (int)__builtin_ctzll(jm);
                         const uint32_t cc = c + (uint32_t)j;
@@ -3021,11 +3059,15 @@ kaneko_coop_kernel(SearchParams p) {
 #ifdef BCHK_DIAG
         // chunk counts of every wave into the acceptor's record
         if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long *>(&p.diag[(size_t)drec * 8 + 3]), dg[3]);
+        if (NW > 1 && wid != kAcceptor && lane == 0) {  // m >= 7: [4] claim, [5] wait cycles of all decoders
+            atomicAdd(reinterpret_cast<unsigned long long *>(&p.diag[(size_t)drec * 8 + 4]), dg[4]);
+            atomicAdd(reinterpret_cast<unsigned long long *>(&p.diag[(size_t)drec * 8 + 5]), dg[5]);
+        }
         if (wid == kAcceptor && lane == 0) {
             dg[6] = __builtin_amdgcn_s_memtime() - t_start;
             dg[7] = cw;
             for (int q = 0; q < 8; ++q)
-                if (q != 3) p.diag[(size_t)drec * 8 + q] = dg[q];
+                if (q != 3 && !(NW > 1 && (q == 4 || q == 5))) p.diag[(size_t)drec * 8 + q] = dg[q];
         }
 #endif
     }

@@ -10,6 +10,6 @@ cd $ROOT
 : > $OUT/${TAG}.jsonl
 for n in 1 2 3 full; do
   if [ $n = full ]; then L=$ROOT/polar-codes-with-bch-kernel_amd/lib/libbchk.so; else L=$ROOT/polar-codes-with-bch-kernel_amd/lib/libbchk_fcut$n.so; fi
-  BCHK_LIB=$L timeout -k 10 200 python bench.py --cpu-seconds 0 --m 8 --t 15 --snr 7 --J 15 --steps 3 --warmup 1 >> $OUT/${TAG}.jsonl 2>> $OUT/${TAG}.err
+  BCHK_CUT_BUILD=1 BCHK_LIB=$L timeout -k 10 200 python bench.py --cpu-seconds 0 --points '' --m 8 --t 15 --snr 7 --J 15 --steps 3 --warmup 1 >> $OUT/${TAG}.jsonl 2>> $OUT/${TAG}.err
   rc=$?; echo "cut $n rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
