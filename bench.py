@@ -121,8 +121,9 @@ def cpu_baseline(args, gpu_rate, bchk):
     kind = "reference"
     if args.J not in (15, -1) or not os.path.exists(exe):
         exe, kind = None, "port"
-    # size the sample from a short probe so the whole leg takes ~cpu_seconds
-    probe = 2000
+    # size the sample from a short probe so the whole leg takes ~cpu_seconds (long codes: a
+    # heavy BCH(255) codeword costs the reference ~1 s at 5 dB, J = 15)
+    probe = 2000 if args.m <= 6 else 64
     if exe:
         procs = args.cpu_procs or host_cores()
 

@@ -558,7 +558,11 @@ __device__ __forceinline__ bool alg_decode_lanes(const uint8_t *__restrict__ ex,
 #pragma unroll
     for (int i = 0; i <= TMAX; ++i) lc[i] = lg[C[i]];
     bool ok = act && (L <= t) && (deg >= 1);
+#if defined(BCHK_SPLIT_CUT)  // experiment builds only (wrong results): Berlekamp-Massey alone
+    ok = ok && lc[0] == 12345;
+#else
     if (ballot(ok)) ok = split_test<M, TMAX>(ex, lg, lc, deg, ok) && ok;
+#endif
 #pragma unroll
     for (int s = 0; s < NW; ++s) E.w[s] = 0;
     for (uint64_t sm = ballot(ok); sm; sm &= sm - 1) {
@@ -712,6 +716,118 @@ __device__ __forceinline__ bool alg_decode_wave(const uint8_t *__restrict__ ex,
         cnt += __popcll(E.w[s]);
     }
     return (L <= t) && (deg >= 1) && (cnt == deg);
+}
+
+// v of lane - 1 within the lane's DPP row of 16 (row_shr:1); the row's lane 0 gets `fill`
+__device__ __forceinline__ int row_shr1(int v, int fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x111, 0xF, 0xF, false);
+}
+
+// Decoder::decode of FOUR test words by one wave (long codes, TMAX <= 15): DPP row r (lanes
+// 16r .. 16r+15) solves word r's key equation with lane j holding coefficient j -- the
+// recurrence of alg_decode_wave, its lane moves and discrepancy XOR kept inside the row --
+// so one chain of dependent LDS lookups serves four words; then each word's Chien search by
+// the whole wave, as alg_decode_wave. Sw4[r] = word r's packed odd syndromes (wave-uniform);
+// Eout (LDS): [r][NW] word r's flipped positions, [4 NW + r] its success.
+template <int M, int TMAX>
+__device__ __forceinline__ void alg_decode_wave4(const uint8_t *__restrict__ ex,
+                                                 const uint16_t *__restrict__ lg,
+                                                 const uint32_t (&Sw4)[4][(TMAX + 3) / 4], int t, int lane,
+                                                 uint64_t *Eout) {
+    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL, NW = Geo<M>::NW, W = (TMAX + 3) / 4;
+    static_assert(TMAX <= 15, "16 coefficients per DPP row");
+    const int r = lane >> 4, j = lane & 15;
+    // lane j of row r: log S_{j+1} (lo) and log S_{j+17} (hi) of word r
+    int lSlo, lShi;
+    {
+        uint32_t wv[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            wv[w] = r == 0 ? Sw4[0][w] : (r == 1 ? Sw4[1][w] : (r == 2 ? Sw4[2][w] : Sw4[3][w]));
+        auto lsq = [&](int q) {
+            const int j1 = q + 1;
+            const int e = __builtin_ctz(j1);
+            const int o = j1 >> e;
+            const int jb = (o - 1) >> 1;
+            uint32_t x = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) x = (w == (jb >> 2)) ? wv[w] : x;
+            const uint32_t so = jb < TMAX ? (x >> (8 * (jb & 3))) & 0xFFu : 0u;
+            const int ls = lg[so];
+            return ls == ZL ? ZL : (int)(((uint32_t)ls << e) % (uint32_t)N);
+        };
+        lSlo = lsq(j);
+        lShi = lsq(j + 16);
+    }
+    const int rowbase = lane & 48;
+    uint32_t C = j == 0 ? 1u : 0u;
+    int lB = j == 0 ? 0 : ZL;
+    int lgam = 0, L = 0;
+    int lsv = j == 0 ? lSlo : ZL;  // lane j: log S_{2k - j + 1} at step k
+    for (int k = 0; k < t; ++k) {
+        const int r2 = 2 * k;
+        const int lC = lg[C];
+        const int top = 2 * k - 1 > 0 ? (2 * k - 1 < TMAX ? 2 * k - 1 : TMAX) : 0;
+        uint32_t d = j <= top ? gf_exp2<M>(ex, lC, lsv) : 0u;
+        d ^= lane_xor<1>(d, lane);
+        d ^= lane_xor<2>(d, lane);
+        d ^= lane_xor<4>(d, lane);
+        d ^= lane_xor<8>(d, lane);
+        const int ld = lg[d];
+        const bool chg = (d != 0u) && (2 * L <= r2);
+        const int lBm1 = row_shr1(lB, ZL);
+        const int lBm2 = row_shr1(lBm1, ZL);
+        const int lCm1 = row_shr1(lC, ZL);
+        int lf = ld - lgam;
+        lf = lf < 0 ? lf + N : lf;
+        lf = d ? lf : ZL;
+        const uint32_t Cn = j ? (C ^ gf_exp2<M>(ex, lf, lBm1)) : C;
+        C = (j > 2 * k + 1 || j > TMAX) ? 0u : Cn;
+        lB = j == 0 ? ZL : (chg ? lCm1 : (j >= 2 ? lBm2 : ZL));
+        L = chg ? r2 + 1 - L : L;
+        lgam = chg ? ld : lgam;
+        if (k + 1 < t) {
+            const int q0 = r2 + 2, q1 = r2 + 1;  // log S_{r2+3}, log S_{r2+2} of the row
+            const int n0 = __shfl(q0 < 16 ? lSlo : lShi, rowbase + (q0 & 15), 64);
+            const int n1 = __shfl(q1 < 16 ? lSlo : lShi, rowbase + (q1 & 15), 64);
+            const int s2 = row_shr1(row_shr1(lsv, ZL), ZL);
+            lsv = j == 0 ? n0 : (j == 1 ? n1 : s2);
+        }
+    }
+    const uint64_t nz = ballot(C != 0u && j <= TMAX && j >= 1);
+    const int ltl = lg[C];
+#pragma unroll
+    for (int w4 = 0; w4 < 4; ++w4) {
+        const uint32_t mr = (uint32_t)(nz >> (16 * w4)) & 0xFFFFu;
+        const int deg = mr ? 31 - __builtin_clz(mr) : 0;
+        const int Lr = (int)rdl((uint32_t)L, 16 * w4);
+        int kk[NW], ik[NW];
+        uint32_t v[NW];
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            const int pos = lane + 64 * s;
+            kk[s] = pos ? N - pos : 0;
+            ik[s] = 0;
+            v[s] = 0;
+        }
+        for (int i = 0; i <= deg; ++i) {
+            const int lti = (int)rdl((uint32_t)ltl, 16 * w4 + i);
+#pragma unroll
+            for (int s = 0; s < NW; ++s) {
+                v[s] ^= gf_exp2<M>(ex, lti, ik[s]);
+                ik[s] += kk[s];
+                ik[s] = ik[s] >= N ? ik[s] - N : ik[s];
+            }
+        }
+        int cnt = 0;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            const uint64_t e = ballot(lane + 64 * s < N && v[s] == 0u);
+            cnt += __popcll(e);
+            if (lane == 0) Eout[w4 * NW + s] = e;
+        }
+        if (lane == 0) Eout[4 * NW + w4] = ((Lr <= t) && (deg >= 1) && (cnt == deg)) ? 1ull : 0ull;
+    }
 }
 
 __device__ __forceinline__ void load_tables(uint8_t *dst, const uint8_t *src, uint32_t bytes) {

@@ -737,12 +737,13 @@ __device__ __forceinline__ void write_outputs(const SearchState<Geo<M>::NW> &S, 
 // at base 0 decodes these patterns again to the same results; none of them is an
 // improvement a second time (l0 <= their l), so the state advances exactly as in the
 // reference. Sets S.done when the codeword's search has ended.
-template <int M, int TMAX>
+template <int M, int TMAX, bool PRE0 = false>
 __device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const Prep<M, TMAX> &P,
                                                const SearchParams &p, const uint8_t *ex,
                                                const uint16_t *lg, const double *as,
                                                const double *ap, int lane,
-                                               int nsel = Geo<M>::N, bool *bail = nullptr) {
+                                               int nsel = Geo<M>::N, bool *bail = nullptr,
+                                               const Mask<Geo<M>::NW> *E0 = nullptr, bool ok0 = false) {
     constexpr int NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
     for (int i = 0; i < kSeqPatterns; ++i) {
         if ((uint64_t)i >= S.bound) {  // the loop ends at its bound (:361)
@@ -754,7 +755,13 @@ __device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const
 #pragma unroll
         for (int w = 0; w < W; ++w) Sw[w] = P.S0[w] ^ rdl(P.Lo[w], i);
         Mask<NW> E;
-        const bool ok = alg_decode_wave<M, TMAX>(ex, lg, Sw, p.t, lane, E);
+        bool ok;
+        if (PRE0 && i == 0) {  // pattern 0 decoded by the caller (alg_decode_wave4)
+            ok = ok0;
+            E = *E0;
+        } else {
+            ok = alg_decode_wave<M, TMAX>(ex, lg, Sw, p.t, lane, E);
+        }
         if (i == 0 && !ok) S.firstOK = false;  // :371
         if (ok) {
 #pragma unroll
@@ -2289,9 +2296,40 @@ kaneko_search_kernel(SearchParams p) {
 // kernel, so it holds fewer registers than the search kernel and keeps more waves in flight
 // to hide the channel loads. A codeword whose search has not ended goes to the exact
 // kernel's queue (one atomic per queued codeword), which starts it from scratch.
+// The hard decision's odd syndromes of codeword cw (prep_syndromes' S0, from the row alone:
+// yH = (2y/s2 > 0), :336-342, Decoder::findSyndromPoly :184-207)
+template <int M, int TMAX>
+__device__ __forceinline__ void hard_syndromes(const SearchParams &p, const uint32_t *col, uint32_t cw, int lane,
+                                               uint32_t (&S0)[Prep<M, TMAX>::W]) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W;
+    double yv[NW];
+    load_row<M>(p, cw, lane, yv);
+#pragma unroll
+    for (int w = 0; w < W; ++w) S0[w] = 0;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const int pos = lane + 64 * s;
+        const double al = (2.0 * yv[s]) / p.s2;
+        if (pos < N && !(al <= 0.0)) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w];
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) S0[w] = wave_xor(S0[w]);
+}
+
 // SEL (no stats record requested, so an exact tie beyond the selection is not observable):
 // the order by prep_select, and the fused counters summed per wave (one set of atomics per
 // wave instead of per codeword).
+// Each wave decodes kFirstPerWave consecutive codewords. Without a stats record their sent
+// words come into LDS, and their decoded words leave it, as one contiguous block of
+// kFirstPerWave rows moved with 8-B accesses (the row of one codeword is n bytes at an odd
+// offset: byte accesses, one per lane per 64 positions, cost the memory pipe more than the
+// bytes); rows not finished here (queued) are left to the search kernel and stored by it.
+constexpr uint32_t kFirstPerWave = 8;
+constexpr int kFirstBlockBytes = 2048;  // kFirstPerWave rows of n <= 255 bytes
+constexpr int kFirstWaveExtra = 2 * kFirstBlockBytes + 256;  // + four words' pattern-0 results
 template <int M, int TMAX, bool SEL>
 __global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4)))
 kaneko_first_kernel(SearchParams p) {
@@ -2302,37 +2340,88 @@ kaneko_first_kernel(SearchParams p) {
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
     const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr int NP = Smem<M, TMAX>::NP, NW = Geo<M>::NW;
+    constexpr int NP = Smem<M, TMAX>::NP, NW = Geo<M>::NW, N = Geo<M>::N;
+    static_assert(kFirstPerWave * N <= kFirstBlockBytes, "a wave's rows fit its block");
     uint8_t *wbase = smem + ((p.td.bytes + 15) & ~15u) + wid * Smem<M, TMAX>::WAVE_BYTES;
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
-    const uint32_t stride = gridDim.x * kWavesPerBlock;
+    // the wave's row blocks (SEL): sent words, decoded words
+    uint8_t *txs = smem + ((p.td.bytes + 15) & ~15u) + kWavesPerBlock * Smem<M, TMAX>::WAVE_BYTES +
+                   wid * kFirstWaveExtra;
+    uint8_t *rss = txs + kFirstBlockBytes;
+    uint64_t *e4s = reinterpret_cast<uint64_t *>(rss + kFirstBlockBytes);  // [4][NW] + ok flags
+    const uint32_t cw0 = (blockIdx.x * kWavesPerBlock + wid) * kFirstPerWave;
+    if (cw0 >= p.count) return;
+    const uint32_t nrows = p.count - cw0 < kFirstPerWave ? p.count - cw0 : kFirstPerWave;
+    const uint32_t nbytes = nrows * (uint32_t)N;
+    // 8-B pieces: row blocks start at a multiple of 8 rows (8 N bytes); the tail of a ragged
+    // last block byte by byte
+    const bool wide = nrows == kFirstPerWave && ((reinterpret_cast<uintptr_t>(p.tx) | reinterpret_cast<uintptr_t>(p.res)) & 7u) == 0;
+    if (SEL && p.cnt) {
+        const uint8_t *src = p.tx + (size_t)cw0 * N;
+        if (wide) {
+            for (uint32_t q = (uint32_t)lane; q < nbytes / 8u; q += 64u)
+                reinterpret_cast<uint64_t *>(txs)[q] = reinterpret_cast<const uint64_t *>(src)[q];
+        } else {
+            for (uint32_t q = (uint32_t)lane; q < nbytes; q += 64u) txs[q] = src[q];
+        }
+    }
     // the next codeword's row is loaded while this one is decoded (its latency hidden)
-    // (and its sent word, for the fused counters at the output step)
+    // (and its sent word, for the fused counters at the output step, with a stats record)
     double ynext[NW];
     TxPre<NW> txnext{{}, false};
-    uint32_t cw = blockIdx.x * kWavesPerBlock + wid;
-    if (cw < p.count) {
-        load_row<M>(p, cw, lane, ynext);
-        txnext = tx_prefetch<M>(p, cw, lane);
-    }
+    load_row<M>(p, cw0, lane, ynext);
+    if (!SEL) txnext = tx_prefetch<M>(p, cw0, lane);
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
-    const uint32_t cw_first = cw;
-    for (; cw < p.count; cw += stride) {
+    uint32_t fin = 0;     // SEL: rows finished here (bit k: codeword cw0 + k)
+    double l0k = 0.0;     // SEL: lane k holds codeword cw0 + k's l0
+    for (uint32_t k = 0; k < nrows; ++k) {
+        const uint32_t cw = cw0 + k;
         double yv[NW];
 #pragma unroll
         for (int s = 0; s < NW; ++s) yv[s] = ynext[s];
         const TxPre<NW> txp = txnext;
-        if (cw + stride < p.count) {
-            load_row<M>(p, cw + stride, lane, ynext);
-            txnext = tx_prefetch<M>(p, cw + stride, lane);
+        if (k + 1 < nrows) {
+            load_row<M>(p, cw + 1, lane, ynext);
+            if (!SEL) txnext = tx_prefetch<M>(p, cw + 1, lane);
         }
 #if defined(BCHK_FIRST_CUT) && BCHK_FIRST_CUT == 1
         // experiment builds only (wrong results, timing of the phases): channel loads
         if (yv[0] + yv[NW - 1] == 12345.0) p.l0[cw] = 0.0;  // keeps the loads
         continue;
 #endif
+        if constexpr (TMAX <= 15) {
+            if ((k & 3u) == 0) {
+                // test pattern 0 of this and the next three words: one four-row key-equation
+                // solve (their rows are read again, from the cache, for the prep)
+                constexpr int W = Prep<M, TMAX>::W;
+                uint32_t *s4s = reinterpret_cast<uint32_t *>(e4s + 5 * NW);  // [4][W]
+#pragma nounroll
+                for (int q = 0; q < 4; ++q) {  // one row at a time (registers)
+                    uint32_t Sq[W];
+                    if (k + (uint32_t)q < nrows) {
+                        hard_syndromes<M, TMAX>(p, col, cw + (uint32_t)q, lane, Sq);
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < W; ++w) Sq[w] = 0;
+                    }
+                    if (lane == 0) {
+#pragma unroll
+                        for (int w = 0; w < W; ++w) s4s[q * W + w] = Sq[w];
+                    }
+                }
+                wave_sync();
+                uint32_t S4[4][W];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w) S4[q][w] = s4s[q * W + w];
+                }
+                alg_decode_wave4<M, TMAX>(ex, lg, S4, p.t, lane, e4s);
+                wave_sync();
+            }
+        }
         Prep<M, TMAX> P;
         int nsel = Geo<M>::N;
         bool selected = false;
@@ -2356,18 +2445,79 @@ kaneko_first_kernel(SearchParams p) {
         SearchState<NW> S;
         init_state<M>(S, p.variant);
         bool bail = false;
-        first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane, nsel, &bail);
+        if constexpr (TMAX <= 15) {
+            Mask<NW> E0;
+#pragma unroll
+            for (int s2 = 0; s2 < NW; ++s2) E0.w[s2] = rdl64(e4s[(k & 3u) * NW + s2], 0);  // uniform (SGPRs)
+            const bool ok0 = uni((int)e4s[4 * NW + (k & 3u)]) != 0;
+            first_patterns<M, TMAX, true>(S, P, p, ex, lg, as, ap, lane, nsel, &bail, &E0, ok0);
+        } else {
+            first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane, nsel, &bail);
+        }
+#if defined(BCHK_FIRST_CUT) && BCHK_FIRST_CUT == 4
+        ap[lane] = S.l0 + (double)(S.done ? 1 : 0) + (double)(bail ? 2 : 0);  // + the first patterns
+        continue;
+#endif
         if (S.done && !bail) {
-            write_outputs<M, TMAX>(S, P, p, cw, lane, txp, SEL ? acc : nullptr);
+            if constexpr (SEL) {
+                // the decoded row into the block (the accepted word: a finished codeword
+                // returned or ran to its bound after an acceptance -- or, never accepted,
+                // keeps the caller's row, which the block then reads back), counters from
+                // the sent words' block (src/dataForPlot.cpp:55-74)
+                uint32_t bit_errors = 0;
+                const bool accp = S.accepted;
+#pragma unroll
+                for (int s2 = 0; s2 < NW; ++s2) {
+                    const int pos = lane + 64 * s2;
+                    if (pos < N) {
+                        uint8_t x;
+                        if (accp) {
+                            x = (uint8_t)(((P.yH.w[s2] ^ S.best.w[s2]) >> lane) & 1ull);
+                        } else {
+                            x = p.res[(size_t)cw * N + pos];
+                        }
+                        rss[k * N + pos] = x;
+                        if (p.cnt) bit_errors += (uint32_t)__popcll(ballot(x != txs[k * N + pos]));
+                    }
+                }
+                if (p.cnt) {
+                    const bool word_variant = p.variant == BCHK_VARIANT_WORD;
+                    const uint64_t iters = S.returned ? S.i_end - 1 : S.i_end;
+                    const uint64_t pro = word_variant ? (uint64_t)(2 * N + 1) : 0ull;
+                    acc[0] += bit_errors ? 1ull : 0ull;
+                    acc[1] += (unsigned long long)bit_errors;
+                    acc[2] += (unsigned long long)S.i_end;
+                    acc[3] += (unsigned long long)(pro + iters * (uint64_t)(N + 6) + S.jsteps + S.impr);
+                    acc[4] += (unsigned long long)(pro + iters * (uint64_t)(N + 1) + S.jsteps);
+                    acc[5] += 1ull;
+                }
+                fin |= 1u << k;
+                l0k = lane == (int)k ? S.l0 : l0k;
+            } else {
+                write_outputs<M, TMAX>(S, P, p, cw, lane, txp);
+            }
         } else if (lane == 0) {
             p.queue_out[atomicAdd(p.qtail, 1u)] = cw;
         }
     }
-    if (SEL && p.cnt && cw_first < p.count && lane == 0) {
-        unsigned long long *c = p.cnt + (size_t)(cw_first % (uint32_t)kCntSlots) * kCntStride;
+    if constexpr (SEL) {
+        wave_sync();
+        uint8_t *dst = p.res + (size_t)cw0 * N;
+        const uint32_t all = (1u << nrows) - 1u;
+        if (fin == all && wide) {
+            for (uint32_t q = (uint32_t)lane; q < nbytes / 8u; q += 64u)
+                reinterpret_cast<uint64_t *>(dst)[q] = reinterpret_cast<const uint64_t *>(rss)[q];
+        } else {
+            for (uint32_t q = (uint32_t)lane; q < nbytes; q += 64u)
+                if ((fin >> (q / (uint32_t)N)) & 1u) dst[q] = rss[q];
+        }
+        if (p.l0 && lane < (int)nrows && ((fin >> lane) & 1u)) p.l0[cw0 + (uint32_t)lane] = l0k;
+        if (p.cnt && lane == 0) {
+            unsigned long long *c = p.cnt + (size_t)(cw0 / kFirstPerWave % (uint32_t)kCntSlots) * kCntStride;
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
-            if (acc[k]) atomicAdd(c + k, acc[k]);
+            for (int q = 0; q < 6; ++q)
+                if (acc[q]) atomicAdd(c + q, acc[q]);
+        }
     }
 }
 
@@ -3233,12 +3383,13 @@ static const void *search_fn() { return reinterpret_cast<const void *>(&kaneko_s
 template <int M, int TMAX, bool TAB>
 static const void *coop_fn() { return reinterpret_cast<const void *>(&kaneko_coop_kernel<M, TMAX, TAB>); }
 
-// codewords per wave of kaneko_first_kernel (grid-stride): amortises the table staging
-constexpr uint32_t kFirstPerWave = 8;
+// kaneko_first_kernel: kFirstPerWave consecutive codewords per wave; its row blocks after
+// the search kernel's LDS layout
 template <int M, int TMAX>
-static hipError_t launch_first_impl(const SearchParams &p, size_t lds, hipStream_t s) {
+static hipError_t launch_first_impl(const SearchParams &p, size_t lds0, hipStream_t s) {
     const uint32_t per_block = kWavesPerBlock * kFirstPerWave;
     const int blocks = (int)((p.count + per_block - 1) / per_block);
+    const size_t lds = lds0 + (size_t)kWavesPerBlock * kFirstWaveExtra;
     if constexpr (first_sel_capable<M, TMAX>()) {
         if (!p.st && !getenv("BCHK_FIRST_FULLSORT")) {
             hipLaunchKernelGGL((kaneko_first_kernel<M, TMAX, true>), dim3(blocks > 0 ? blocks : 1),

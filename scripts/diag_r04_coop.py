@@ -32,5 +32,10 @@ for name, lim, fast, an in (("exact-only", "0", False, True), ("coop-heavy", "1"
             ref = (res, l0, st)
         else:
             print("  equal to exact-only:", bool(np.array_equal(res, ref[0]) and np.array_equal(st, ref[2])), flush=True)
+            bad = np.flatnonzero((res != ref[0]).any(axis=1) | (st != ref[2]))
+            for r in bad[:4]:
+                print("   row", int(r), "exact", {k: int(ref[2][k][r]) for k in ("decodes", "jsteps", "improvements", "flags")},
+                      "this", {k: int(st[k][r]) for k in ("decodes", "jsteps", "improvements", "flags")},
+                      "l0", float(ref[1][r]), float(l0[r]), flush=True)
     except Exception as e:
         print(name, "FAILED", f"{time.time() - t0:.2f}s", e, flush=True)
