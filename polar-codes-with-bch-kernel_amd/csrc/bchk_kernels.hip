@@ -2330,8 +2330,11 @@ __device__ __forceinline__ void hard_syndromes(const SearchParams &p, const uint
 constexpr uint32_t kFirstPerWave = 8;
 constexpr int kFirstBlockBytes = 2048;  // kFirstPerWave rows of n <= 255 bytes
 constexpr int kFirstWaveExtra = 2 * kFirstBlockBytes + 256;  // + four words' pattern-0 results
+#ifndef BCHK_LONGFIRST_WPE  // experiment builds set it (waves per SIMD the allocation targets)
+#define BCHK_LONGFIRST_WPE 4
+#endif
 template <int M, int TMAX, bool SEL>
-__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(kWaveSize * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(BCHK_LONGFIRST_WPE)))
 kaneko_first_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
