@@ -2540,7 +2540,16 @@ kaneko_first_kernel(SearchParams p) {
 #ifndef BCHK_COOP_SLOTS
 #define BCHK_COOP_SLOTS 48
 #endif
-constexpr int kCoopSlotsMax = 128;
+#ifndef BCHK_LONG_SLOTS  // experiment builds vary the long-code ring and tail claims
+#define BCHK_LONG_SLOTS 128
+#endif
+#ifndef BCHK_LONG_TAIL
+#define BCHK_LONG_TAIL 0
+#endif
+#ifndef BCHK_LONG_TAIL_CLAIM
+#define BCHK_LONG_TAIL_CLAIM 4
+#endif
+constexpr int kCoopSlotsMax = BCHK_LONG_SLOTS > 128 ? BCHK_LONG_SLOTS : 128;
 // Long codes (m >= 7): a decoder wave claims kLongClaim chunks at once and decodes only
 // their patterns that can still matter -- the ones skip_lane does not rule out -- packed 64
 // to a round (lane i no longer decodes pattern base + i). At 5 dB on BCH(255,139,31) the
@@ -2553,7 +2562,7 @@ constexpr int kCoopSlotsMax = 128;
 // published loop bound waits -- the bound may rise again -- until the codeword is done or
 // the bound passes it.
 constexpr int kLongClaim = 8;
-constexpr int kLongSlots = 128;
+constexpr int kLongSlots = BCHK_LONG_SLOTS;
 constexpr int kLongRec = 2;
 template <int NW>
 constexpr int coop_slots() { return NW == 1 ? BCHK_COOP_SLOTS : kLongSlots; }
@@ -2682,7 +2691,7 @@ __device__ __forceinline__ void mask_flip(Mask<NW> &m, int p) {
     for (int s = 0; s < NW; ++s) m.w[s] ^= (uint64_t)((p >> 6) == s) << (p & 63);
 }
 
-// A decoder wave's claim of kLongClaim chunks c .. c + 7 (m >= 7; c a multiple of 8): the
+// A decoder wave's claim of nch <= kLongClaim chunks c .. c + nch - 1 (m >= 7): the
 // patterns skip_lane leaves, packed 64 per round (the k-th of them in lane k), decoded; each
 // success goes, in pattern order, into its chunk's success mask and -- when it is a strict
 // running minimum of l below l0 as published (the candidates of the dense ring) -- into the
@@ -2693,10 +2702,10 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
                                                   double l0r, uint64_t skey, int t, const uint8_t *ex,
                                                   const uint16_t *lg, const uint64_t *chien, const double *ap,
                                                   void *wscratch, LongSlot<Geo<M>::NW> *ring, CoopCtl *ctl,
-                                                  int lane) {
+                                                  int lane, uint32_t nch) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W, G = kLongClaim;
     constexpr int NB = N < 31 ? N : 31;
-    static_assert(G == 8, "pattern bits 6..8 select the chunk within a claim");
+    static_assert(G == 8, "lanes 0..7 form the claim's chunk syndromes");
     // per-wave LDS scratch (the wave's sorted-|alpha| slice, used by the acceptor only):
     // the chunks' pattern masks and the syndromes of the hard decision ^ pattern bits >= 6
     uint64_t *actl = reinterpret_cast<uint64_t *>(wscratch);
@@ -2706,10 +2715,11 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const uint64_t b = 64ull * (uint64_t)(c + (uint32_t)g);
-        const uint64_t a = (b < capc && b < bnd) ? ballot(!skip_lane(skey, b + (uint64_t)lane, t)) : 0ull;
+        const bool own = (uint32_t)g < nch;  // chunks past nch belong to later claims
+        const uint64_t a = (own && b < capc && b < bnd) ? ballot(!skip_lane(skey, b + (uint64_t)lane, t)) : 0ull;
         if (lane == 0) actl[g] = a;
         pre[g + 1] = pre[g] + __popcll(a);
-        if (b < capc && lane == 0) {  // the slot's running state (the ring space is ours)
+        if (own && b < capc && lane == 0) {  // the slot's running state (the ring space is ours)
             LongSlot<NW> &S = ring[(c + (uint32_t)g) % kLongSlots];
             S.okm = 0ull;
             S.ncand = 0u;
@@ -2797,7 +2807,7 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const uint32_t cg = c + (uint32_t)g;
-        if (64ull * cg >= capc) break;  // never read by the acceptor
+        if ((uint32_t)g >= nch || 64ull * cg >= capc) break;  // not ours / never read by the acceptor
         if (lane == 0) lds_st(&ctl->ready[cg % kLongSlots], cg + 1u);
     }
     wave_sync();
@@ -2938,9 +2948,19 @@ kaneko_coop_kernel(SearchParams p) {
         if (NW > 1 && wid != kAcceptor) {
             // ------------------------------------------------ decoder, m >= 7 (packed)
             for (bool fin = false; !fin;) {
-                uint32_t c = 0;
-                if (lane == 0) c = atomicAdd(&ctl->next, (uint32_t)kLongClaim);
+                uint32_t c = 0, nch = (uint32_t)kLongClaim;
+                if (lane == 0) {
+                    // the last BCHK_LONG_TAIL chunks below the published bound in smaller
+                    // claims: the codeword ends with its slowest claim
+                    if (BCHK_LONG_TAIL > 0) {
+                        const uint64_t bch = (lds_ld64(&ctl->bound) + 63ull) >> 6;
+                        if ((uint64_t)lds_ld(&ctl->next) + (uint64_t)BCHK_LONG_TAIL >= bch)
+                            nch = (uint32_t)BCHK_LONG_TAIL_CLAIM;
+                    }
+                    c = atomicAdd(&ctl->next, nch);
+                }
                 c = (uint32_t)__shfl((int)c, 0, 64);
+                nch = (uint32_t)__shfl((int)nch, 0, 64);
                 // wait for ring space, and while the claim lies past the published bound (it
                 // may rise again) or the cap: the codeword's end (done) releases the wave;
                 // dense requests are served meanwhile
@@ -2979,7 +2999,7 @@ kaneko_coop_kernel(SearchParams p) {
                 int rounds = 0;
                 if constexpr (NW > 1)
                     rounds = long_decode_claim<M, TMAX>(P, c, capc, ~0ull, l0r, skey, p.t, ex, lg, chien, ap, as, lring,
-                                                        ctl, lane);
+                                                        ctl, lane, nch);
 #ifdef BCHK_DIAG
                 dg[3] += (unsigned long long)rounds;  // m >= 7: decode rounds of 64 packed patterns
                 dg[4] += __builtin_amdgcn_s_memtime() - tw1;  // m >= 7 decoders: cycles in claims
