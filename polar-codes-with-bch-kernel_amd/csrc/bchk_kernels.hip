@@ -2540,11 +2540,15 @@ kaneko_first_kernel(SearchParams p) {
 #ifndef BCHK_COOP_SLOTS
 #define BCHK_COOP_SLOTS 48
 #endif
-#ifndef BCHK_LONG_SLOTS  // experiment builds vary the long-code ring and tail claims
-#define BCHK_LONG_SLOTS 128
+// Long-code ring slots and tail claims (experiment builds vary them; BCH(255,139,31), 2^20,
+// cooperative kernel at 5 dB J=15 / 6 dB J=inf: 128 slots 85.1 / 11.0 ms, 256 slots 82.9 /
+// 9.9, + 4-chunk claims in the last 60 chunks 81.1-81.6 / 9.8-9.9, 384 slots 81.1 / 9.7;
+// profiles/r04_long/coop_ring*.jsonl)
+#ifndef BCHK_LONG_SLOTS
+#define BCHK_LONG_SLOTS 256
 #endif
 #ifndef BCHK_LONG_TAIL
-#define BCHK_LONG_TAIL 0
+#define BCHK_LONG_TAIL 60
 #endif
 #ifndef BCHK_LONG_TAIL_CLAIM
 #define BCHK_LONG_TAIL_CLAIM 4
