@@ -434,8 +434,10 @@ def stream_skip(k, n, state, words):
 
 
 def stream_sync(k, n, state, offset, limit):
-    """The first word start at or after `offset` draws from word start `state`, without parsing
-    the draws before it: (draws from state, engine state), or None when unresolved."""
+    """A word start in [offset, offset + limit) draws from word start `state` that depends only
+    on (state, offset, limit) -- where every parse possible at `offset` has merged, not
+    necessarily the first start at or after it -- found without parsing the draws before
+    `offset`: (draws from state, engine state), or None when unresolved."""
     off, st = C.c_uint64(), C.c_uint64()
     rc = lib().bchk_stream_sync(k, n, state, offset, limit, C.byref(off), C.byref(st))
     if rc == 1:
