@@ -2551,7 +2551,7 @@ kaneko_first_kernel(SearchParams p) {
 #define BCHK_LONG_TAIL 60
 #endif
 #ifndef BCHK_LONG_TAIL_CLAIM
-#define BCHK_LONG_TAIL_CLAIM 4
+#define BCHK_LONG_TAIL_CLAIM 2
 #endif
 constexpr int kCoopSlotsMax = BCHK_LONG_SLOTS > 128 ? BCHK_LONG_SLOTS : 128;
 // Long codes (m >= 7): a decoder wave claims kLongClaim chunks at once and decodes only
@@ -2565,7 +2565,15 @@ constexpr int kCoopSlotsMax = BCHK_LONG_SLOTS > 128 ? BCHK_LONG_SLOTS : 128;
 // chunk), by a decoder wave into the one dense result buffer. A claim that lies past the
 // published loop bound waits -- the bound may rise again -- until the codeword is done or
 // the bound passes it.
-constexpr int kLongClaim = 8;
+// Chunks per decoder claim (experiment builds vary it). BCH(255,139,31), 2^20, cooperative
+// kernel at 5 dB J=15 / 6 dB J=inf: 16 chunks 96.6 / 12.0 ms, 8: 81.7 / 9.9, 4: 78.1 / 9.5
+// (77.4 / 9.5 on a second box), 2: 75.6 / 9.5 (profiles/r04_long/coop_claim_size_variants*.jsonl)
+#ifndef BCHK_LONG_CLAIM
+#define BCHK_LONG_CLAIM 2
+#endif
+constexpr int kLongClaim = BCHK_LONG_CLAIM;
+static_assert(kLongClaim >= 2 && kLongClaim <= 16 && (kLongClaim & (kLongClaim - 1)) == 0 &&
+                  BCHK_LONG_TAIL_CLAIM <= kLongClaim, "claim sizes");
 constexpr int kLongSlots = BCHK_LONG_SLOTS;
 constexpr int kLongRec = 2;
 template <int NW>
@@ -2709,7 +2717,7 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
                                                   int lane, uint32_t nch) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W, G = kLongClaim;
     constexpr int NB = N < 31 ? N : 31;
-    static_assert(G == 8, "lanes 0..7 form the claim's chunk syndromes");
+    static_assert(G <= 64 && (G & (G - 1)) == 0, "lanes 0..G-1 form the claim's chunk syndromes");
     // per-wave LDS scratch (the wave's sorted-|alpha| slice, used by the acceptor only):
     // the chunks' pattern masks and the syndromes of the hard decision ^ pattern bits >= 6
     uint64_t *actl = reinterpret_cast<uint64_t *>(wscratch);
@@ -2730,11 +2738,11 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
             S.run = l0r;
         }
     }
-    {   // lane g < 8: the syndrome of pattern bits >= 6 for chunk c + g
+    {   // lane g < G: the syndrome of pattern bits >= 6 for chunk c + g
         uint32_t h[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) h[w] = P.S0[w];
-        const uint32_t hb = (c + (uint32_t)(lane & 7)) << 6;
+        const uint32_t hb = (c + (uint32_t)(lane & (G - 1))) << 6;
         for (int b = 6; b < NB; ++b) {
 #pragma unroll
             for (int w = 0; w < W; ++w) {
