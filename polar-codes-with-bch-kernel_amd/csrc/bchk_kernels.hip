@@ -2567,12 +2567,13 @@ constexpr int kCoopSlotsMax = BCHK_LONG_SLOTS > 128 ? BCHK_LONG_SLOTS : 128;
 // the bound passes it.
 // Chunks per decoder claim (experiment builds vary it). BCH(255,139,31), 2^20, cooperative
 // kernel at 5 dB J=15 / 6 dB J=inf: 16 chunks 96.6 / 12.0 ms, 8: 81.7 / 9.9, 4: 78.1 / 9.5
-// (77.4 / 9.5 on a second box), 2: 75.6 / 9.5 (profiles/r04_long/coop_claim_size_variants*.jsonl)
+// (77.4 / 9.5 on a second box), 2: 75.6 / 9.5, 1: 82.3 / 11.5
+// (profiles/r04_long/coop_claim_size_variants*.jsonl)
 #ifndef BCHK_LONG_CLAIM
 #define BCHK_LONG_CLAIM 2
 #endif
 constexpr int kLongClaim = BCHK_LONG_CLAIM;
-static_assert(kLongClaim >= 2 && kLongClaim <= 16 && (kLongClaim & (kLongClaim - 1)) == 0 &&
+static_assert(kLongClaim >= 1 && kLongClaim <= 16 && (kLongClaim & (kLongClaim - 1)) == 0 &&
                   BCHK_LONG_TAIL_CLAIM <= kLongClaim, "claim sizes");
 constexpr int kLongSlots = BCHK_LONG_SLOTS;
 constexpr int kLongRec = 2;
