@@ -222,6 +222,11 @@ int bchk_tail_count(bchk_ctx *ctx, uint64_t *to_tail);
  * candidate within the tightened bound, then the candidates), [3] exact chunks of [2],
  * [4] enumeration steps (64 nodes each) summed, [5] their maximum over codewords. */
 int bchk_tail_stats(bchk_ctx *ctx, uint64_t *out6);
+/* The last call's cooperative-kernel counters (m >= 7): [0] chunks decoded again densely on
+ * the acceptor's request (more candidates than a ring slot keeps; BCHK_LONG_REC=0..2 in the
+ * environment at bchk_create sets the records per slot, default 2), [1] heavy codewords the
+ * cooperative kernel started. */
+int bchk_coop_stats(bchk_ctx *ctx, uint64_t *out2);
 /* Diagnostics (context created with BCHK_TAIL_DIAG=1 in the environment): the last call's
  * per-codeword analytic-tail records, 8 u64 each -- codeword, cycles of prep, of the exact
  * chunks, of the plan, enumeration steps, mode | reason << 8 | split chunks << 16, cycles

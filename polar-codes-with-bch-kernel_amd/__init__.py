@@ -34,7 +34,7 @@ EXPORTS = (
     "bchk_generate_host", "bchk_generate_host_draws", "bchk_generate_device", "bchk_sweep_device", "bchk_rng_jump", "bchk_sweep_block", "bchk_sweep_range", "bchk_stream_skip",
     "bchk_stream_sync", "bchk_sweep", "bchk_sync", "bchk_stream", "bchk_profile",
     "bchk_profile_read", "bchk_profile_read_stages", "bchk_path_counts", "bchk_tail_count",
-    "bchk_tail_stats", "bchk_tail_diag_read", "bchk_tail_prof_read", "bchk_set_fast_path", "bchk_set_analytic",
+    "bchk_tail_stats", "bchk_coop_stats", "bchk_tail_diag_read", "bchk_tail_prof_read", "bchk_set_fast_path", "bchk_set_analytic",
     "bchk_set_chunk_limit", "bchk_set_syndrome_table",
     "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_polar_create", "bchk_polar_create_kdir",
     "bchk_polar_destroy", "bchk_polar_params", "bchk_polar_decode_host", "bchk_polar_decode_device",
@@ -126,6 +126,7 @@ def lib():
     L.bchk_path_counts.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)]
     L.bchk_tail_count.argtypes = [vp, C.POINTER(u64)]
     L.bchk_tail_stats.argtypes = [vp, C.POINTER(u64)]
+    L.bchk_coop_stats.argtypes = [vp, C.POINTER(u64)]
     L.bchk_tail_diag_read.argtypes = [vp, C.POINTER(u64), sz, C.POINTER(u64)]
     L.bchk_tail_prof_read.argtypes = [vp, C.POINTER(u64), sz]
     L.bchk_profile_read_stages.argtypes = [vp, C.POINTER(dbl), C.POINTER(u64)]
@@ -328,6 +329,13 @@ class KanekoKernelProcessor:
         enumeration steps, max steps per codeword]."""
         a = (C.c_uint64 * 6)()
         _check(lib().bchk_tail_stats(self._h, a))
+        return list(a)
+
+    def coop_stats(self):
+        """Last call's cooperative-kernel counters (m >= 7): [dense re-decodes served,
+        heavy codewords started]."""
+        a = (C.c_uint64 * 2)()
+        _check(lib().bchk_coop_stats(self._h, a))
         return list(a)
 
     def tail_diag(self, items=65536):

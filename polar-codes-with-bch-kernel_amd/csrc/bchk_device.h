@@ -140,6 +140,11 @@ struct SearchParams {
     // delay of its second half in cycles (0: none)
     uint32_t fast_blocks;
     uint32_t fast_stagger;
+    // cooperative kernel, m >= 7: candidate records a ring slot keeps (0..2; a chunk with more
+    // is decoded again densely on the acceptor's request), and its counters (null = off):
+    // [0] dense re-decodes served, [1] heavy codewords started
+    int32_t long_rec;
+    uint32_t *coop_stats;
 };
 constexpr int kCntSlots = 512;
 constexpr int kCntStride = 16;  // u64 per slot: one 128-B line

@@ -394,6 +394,8 @@ struct bchk_ctx {
     bool use_fast = true;
     size_t lds_fast = 0, lds_coop = 0;
     int grid_coop = 0, grid_coop_tab = 0;
+    int32_t long_rec = 2;      // cooperative kernel (m >= 7): candidate records per ring slot
+    uint64_t last_coop_stats[2] = {0, 0};
     uint32_t chunk_limit = 8;  // exact steps before a hand-off (measured best over 4-6 dB, J = 15 / inf)
     DevBuf diag;
     // One decode pipeline per sub-batch: its work queues, control words (one 128-B line
@@ -475,7 +477,8 @@ constexpr size_t kCtrlBytes = 46 * 128;
 constexpr int kHeavyTail = 32 * 9, kHeavyHead = 32 * 10, kHeavyTail2 = 32 * 11,
               kHeavyHead2 = 32 * 12, kExactDone = 32 * 13, kL1Tail = 32 * 22, kTailHeads = 32 * 23,
               kTailDone = 32 * 31, kTailStats = 32 * 39, kNoneTail = 32 * 40, kNoneHead = 32 * 41,
-              kL1Back = 32 * 42, kL1BackHead = 32 * 43, kQFront = 32 * 44, kQBack = 32 * 45;
+              kL1Back = 32 * 42, kL1BackHead = 32 * 43, kQFront = 32 * 44, kQBack = 32 * 45,
+              kCoopStats = kTailStats + 8;  // line 39, words 8-9: cooperative-kernel counters
 #ifdef BCHK_DIAG
 constexpr int kDiagCount = 32 * 21;
 #endif
@@ -592,6 +595,8 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
     p.exact_total = fast ? ctrl : nullptr;  // the fast path's queue length
     p.heavy_big = kHeavyBig;
     p.chunk_limit = c->chunk_limit;
+    p.long_rec = c->long_rec;
+    p.coop_stats = ctrl + kCoopStats;
     p.analytic = 0;
     if (c->use_table) p.tab = c->tab;
 #ifdef BCHK_DIAG
@@ -871,6 +876,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     if (getenv("BCHK_NO_TABLE")) c->use_table = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);
+    if (const char *lr = getenv("BCHK_LONG_REC")) c->long_rec = std::max(0, std::min(2, atoi(lr)));
     if (const char *cc = getenv("BCHK_COOP_CONCURRENT")) c->coop_concurrent = atoi(cc) != 0;
     if (getenv("BCHK_NO_ANALYTIC")) c->analytic = false;
     if (getenv("BCHK_TAIL_DIAG")) c->tail_diag_on = true;
@@ -1486,6 +1492,14 @@ int bchk_tail_stats(bchk_ctx *c, uint64_t *out6) {
     return 0;
 }
 
+int bchk_coop_stats(bchk_ctx *c, uint64_t *out2) {
+    if (!c || !out2) return fail(BCHK_EINVAL, "NULL argument");
+    uint64_t a = 0, b = 0;
+    if (int rc = bchk_path_counts(c, &a, &b)) return rc;
+    for (int k = 0; k < 2; ++k) out2[k] = c->last_coop_stats[k];
+    return 0;
+}
+
 int bchk_path_counts(bchk_ctx *c, uint64_t *to_exact, uint64_t *to_coop) {
     if (!c) return fail(BCHK_EINVAL, "ctx is NULL");
     // the last call's counts, summed over its pipelines (a pipeline the call did not use
@@ -1493,6 +1507,7 @@ int bchk_path_counts(bchk_ctx *c, uint64_t *to_exact, uint64_t *to_coop) {
     uint64_t v[2] = {0, 0};
     c->last_tail = 0;
     for (auto &x : c->last_tail_stats) x = 0;
+    for (auto &x : c->last_coop_stats) x = 0;
     for (int k = 0; k < c->last_pipes && k < (int)c->pipes.size(); ++k) {
         const bchk_ctx::Pipe &P = c->pipes[k];
         if (!P.ctrl.p) continue;
@@ -1502,6 +1517,7 @@ int bchk_path_counts(bchk_ctx *c, uint64_t *to_exact, uint64_t *to_coop) {
         v[0] += h[0];
         v[1] += (uint64_t)h[kHeavyTail] + h[kHeavyTail2];
         c->last_tail += h[kL1Tail];
+        for (int q = 0; q < 2; ++q) c->last_coop_stats[q] += h[kCoopStats + q];
         for (int q = 0; q < 6; ++q)
             c->last_tail_stats[q] = q == 5 ? std::max<uint64_t>(c->last_tail_stats[q], h[kTailStats + q])
                                            : c->last_tail_stats[q] + h[kTailStats + q];

@@ -2715,7 +2715,7 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
                                                   double l0r, uint64_t skey, int t, const uint8_t *ex,
                                                   const uint16_t *lg, const uint64_t *chien, const double *ap,
                                                   void *wscratch, LongSlot<Geo<M>::NW> *ring, CoopCtl *ctl,
-                                                  int lane, uint32_t nch) {
+                                                  int lane, uint32_t nch, int lrec) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W, G = kLongClaim;
     constexpr int NB = N < 31 ? N : 31;
     static_assert(G <= 64 && (G & (G - 1)) == 0, "lanes 0..G-1 form the claim's chunk syndromes");
@@ -2805,7 +2805,7 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
                     S.ncand = slot_n + 1u;
                 }
             }
-            if (cand && slot_n < (uint32_t)kLongRec && lane == L) {
+            if (cand && slot_n < (uint32_t)lrec && lane == L) {
                 LongRec<NW> &R = S.rec[slot_n];
 #pragma unroll
                 for (int s2 = 0; s2 < NW; ++s2) R.diff[s2] = d.w[s2];
@@ -2855,6 +2855,7 @@ __device__ __forceinline__ bool long_serve_redo(const Prep<M, TMAX> &P, const Se
     if (lane == 0) dn->okm = okm;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) lds_st(&ctl->redo_done, r);
+    if (lane == 0 && p.coop_stats) atomicAdd(p.coop_stats, 1u);
     return true;
 }
 
@@ -2908,11 +2909,12 @@ kaneko_coop_kernel(SearchParams p) {
             ctl->redo_done = 0;
             ctl->go = 0;
         }
-        if (threadIdx.x < kCoopSlots) ctl->ready[threadIdx.x] = 0;
+        for (uint32_t k = threadIdx.x; k < (uint32_t)kCoopSlots; k += blockDim.x) ctl->ready[k] = 0;
         __syncthreads();
         const uint32_t item = ctl->item;
         if (item == kEmptySlot) return;
         if (item >= p.count) continue;  // never a valid slot value: no access outside the batch
+        if (threadIdx.x == 0 && p.coop_stats) atomicAdd(p.coop_stats + 1, 1u);
         const uint32_t cw = item;
 #ifdef BCHK_DIAG
         const uint32_t drec = ctl->drec;  // this codeword's diagnostic record
@@ -2955,7 +2957,15 @@ kaneko_coop_kernel(SearchParams p) {
                     lds_st(&ctl->go, 1u);
                 }
             } else {
-                for (uint32_t sp = 0; !lds_ld(&ctl->go) && ++sp < kSpinLimit;) __builtin_amdgcn_s_sleep(2);
+                uint32_t sp = 0;
+                while (!lds_ld(&ctl->go) && ++sp < kSpinLimit) __builtin_amdgcn_s_sleep(2);
+                if (sp >= kSpinLimit) {  // never expected: fail the codeword, no hang
+                    if (lane == 0) {
+                        flag_fault(p, kFaultCoopRing);
+                        lds_st(&ctl->done, 1u);
+                    }
+                    wave_sync();
+                }
             }
         }
         if (NW > 1 && wid != kAcceptor) {
@@ -3012,7 +3022,7 @@ kaneko_coop_kernel(SearchParams p) {
                 int rounds = 0;
                 if constexpr (NW > 1)
                     rounds = long_decode_claim<M, TMAX>(P, c, capc, ~0ull, l0r, skey, p.t, ex, lg, chien, ap, as, lring,
-                                                        ctl, lane, nch);
+                                                        ctl, lane, nch, p.long_rec);
 #ifdef BCHK_DIAG
                 dg[3] += (unsigned long long)rounds;  // m >= 7: decode rounds of 64 packed patterns
                 dg[4] += __builtin_amdgcn_s_memtime() - tw1;  // m >= 7 decoders: cycles in claims
@@ -3149,7 +3159,7 @@ kaneko_coop_kernel(SearchParams p) {
                         const uint64_t base = 64ull * cc;
                         if (base >= S.bound || base >= capc) { cdone = cc; break; }
                         const LongSlot<NW> &sl = lring[cc % kLongSlots];
-                        if (sl.ncand > (uint32_t)kLongRec) {
+                        if (sl.ncand > (uint32_t)p.long_rec) {
                             // more candidates than the slot holds: a decoder wave decodes the
                             // chunk densely for us (all earlier chunks are consumed, so no
                             // decoder is waiting on us for it)

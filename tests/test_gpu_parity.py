@@ -653,3 +653,69 @@ def test_config5_bch255_batch_heavy_rows_match_exact_path_and_oracle():
                           rng.choice(np.setdiff1d(np.arange(B), heavy), 128, replace=False)])
     r2, l2, s2, a2 = Oracle(8, 15).kaneko_batch(y[idx], J=15)
     check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, a[0][idx], a[1][idx], st[idx])
+
+
+def _ctx_env(m, t, J, **env):
+    """A context created with extra environment knobs (read at bchk_create)."""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return load().KanekoKernelProcessor(m, t, J=J)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_bch127_t10_heavy_rows_match_exact_path_and_oracle():
+    # BCH(127,57,21) (m = 7, t = 10: three syndrome words, the code whose single-call-site
+    # cooperative decoder went wrong in round 4) at 5 dB, J = 15, where ~0.1 % of the words run
+    # to the 2^15 - 1 bound in the cooperative kernel: every row equals the exact-only path,
+    # every row past the first pass's chunks and 1024 others equal the oracle (reference
+    # loop: src/KanekoKernelProcessor.cpp:361-405)
+    F = load()
+    d = dec(7, 10, J=15)
+    ex = dec(7, 10, J=15, path="exact-only")
+    B = 1 << 16
+    _, y, _ = d.generate(5.0, B, seed=127)
+    a = d.decode(y)
+    to_coop = d.path_counts()[1]
+    b = ex.decode(y)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+    np.testing.assert_array_equal(a[2], b[2])
+    st = a[2]
+    assert not np.any(st["flags"] & F.F_TRUNCATED)
+    heavy = np.flatnonzero(st["decodes"] > 8 * 64)
+    assert heavy.size >= 16 and to_coop >= heavy.size and (st["decodes"] == 32767).sum() >= 8
+    rng = np.random.default_rng(5)
+    idx = np.unique(np.concatenate([heavy, rng.choice(B, 1024, replace=False)]))
+    r2, l2, s2, a2 = Oracle(7, 10).kaneko_batch(y[idx], J=15)
+    check_against(r2, l2, s2[:, 0], s2[:, 1], s2[:, 2], a2, a[0][idx], a[1][idx], st[idx])
+    print(f"\nBCH(127,57,21) 5 dB J=15: {to_coop} cooperative, {heavy.size} heavy rows vs the oracle")
+
+
+@pytest.mark.parametrize("long_rec", [0, 1])
+def test_long_code_dense_redecode_handshake(long_rec):
+    # The cooperative kernel's dense re-decode (a chunk with more candidates than its ring
+    # slot keeps is decoded again by a decoder wave on the acceptor's request: long_serve_redo
+    # and the redo / redo_done handshake) forced on by keeping 0 or 1 records per slot: the
+    # requests are served (counted) and every row still equals the exact-only path
+    m, t = 8, 15
+    d = _ctx_env(m, t, 15, BCHK_LONG_REC=long_rec)
+    try:
+        ex = dec(m, t, J=15, path="exact-only")
+        B = 1 << 15
+        _, y, _ = d.generate(5.0, B, seed=59)
+        a = d.decode(y)
+        served, started = d.coop_stats()
+        b = ex.decode(y)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+        np.testing.assert_array_equal(a[2], b[2])
+        assert started >= 100 and served >= started, (served, started)
+        print(f"\nlong_rec {long_rec}: {started} cooperative codewords, {served} dense re-decodes")
+    finally:
+        d.close()

@@ -165,6 +165,50 @@ def test_bench_step_matches_oracle(snr):
           f" (heavy {len(heavy)}); counters {cnt.tolist()}")
 
 
+def test_config5_bench_step_jinf_matches_oracle():
+    # Config 5's 6 dB J = inf bench line (bench.py --m 8 --t 15 --snr 6 --J -1): the bench's own
+    # 2^20 BCH(255,139,31) words through the bench's fused call. Every row against the
+    # exact-only path (one wave per codeword, every pattern in order), and every row that left
+    # the first-pattern kernel (decodes > 4: the search / cooperative kernels' rows, including
+    # the uncapped ~2^17-decode codeword that dominates the step) plus 8192 others against the
+    # oracle (src/KanekoKernelProcessor.cpp:361-405, the shipped non-monotone bound).
+    import torch
+    F = load()
+    m, t, Jinf, snr = 8, 15, -1, 6.0
+    d = F.KanekoKernelProcessor(m, t, J=Jinf)
+    old = os.environ.get("BCHK_CHUNK_LIMIT")
+    os.environ["BCHK_CHUNK_LIMIT"] = "0"
+    try:
+        ex = F.KanekoKernelProcessor(m, t, J=Jinf)
+    finally:
+        os.environ.pop("BCHK_CHUNK_LIMIT")
+        if old is not None:
+            os.environ["BCHK_CHUNK_LIMIT"] = old
+    ex.set_fast_path(False)
+    try:
+        tx, y = rank_words(d, snr, 0, 1)
+        dy, dtx = torch.from_numpy(y).cuda(), torch.from_numpy(tx).cuda()
+        res, l0, cnt = bench_step(d, dy, dtx, B)
+        to_exact, to_coop = d.path_counts()
+        sres, sl0, st = stats_run(ex, dy, B)
+        np.testing.assert_array_equal(sres, res)
+        np.testing.assert_array_equal(sl0.view(np.uint64), l0.view(np.uint64))
+        assert not np.any(st["flags"] & (F.F_TIE | F.F_TRUNCATED))
+        np.testing.assert_array_equal(cnt, counters_from(tx, res, st["decodes"], st["comparisons"], st["sums"]))
+        heavy = np.flatnonzero(st["decodes"] > 4)
+        big = int(st["decodes"].max())
+        assert to_coop >= 1 and big > 8 * CHUNK and (st["decodes"] > 5000).sum() >= 1
+        rng = np.random.default_rng(13)
+        rows = np.unique(np.concatenate([heavy, rng.choice(B, 8192, replace=False)]))
+        r2, l2, s2, a2 = Oracle(m, t).kaneko_batch(y[rows], J=Jinf)
+        assert_rows_equal_oracle(rows, res, l0, st, r2, l2, s2, a2)
+        print(f"\nBCH(255,139,31) 6 dB J=inf: to_exact {to_exact} to_coop {to_coop}; oracle rows {len(rows)}"
+              f" (decodes > 4: {len(heavy)}, > 5000: {int((st['decodes'] > 5000).sum())}, max {big})")
+    finally:
+        d.close()
+        ex.close()
+
+
 def test_config4_batch_equals_eight_shards():
     # BASELINE config 4: 2^23 words = the eight ranks' 2^20 jump-ahead shards. One call over
     # all of them (one GPU) == the eight shard calls (what eight GPUs run), row for row, and
