@@ -136,10 +136,12 @@ struct SearchParams {
     // cnt_reduce_kernel folds into the caller's totals
     const uint8_t *tx;
     unsigned long long *cnt;
-    // fast kernel (bchk_fast.hip), experiment: blocks of the first round and the start
-    // delay of its second half in cycles (0: none)
-    uint32_t fast_blocks;
-    uint32_t fast_stagger;
+    // fast ring kernel (bchk_fast.hip): waves per workgroup (0: all 16 -- 1 loader + 15
+    // compute; fewer leave room for a concurrent kernel), and experiment modes (0: normal;
+    // 1: the loader publishes slots without loading them, 2: compute waves only read their
+    // slot -- timing builds of the two halves, wrong results)
+    uint32_t fast_waves;
+    uint32_t fast_mode;
     // cooperative kernel, m >= 7: candidate records a ring slot keeps (0..2; a chunk with more
     // is decoded again densely on the acceptor's request), and its counters (null = off):
     // [0] dense re-decodes served, [1] heavy codewords started

@@ -76,6 +76,22 @@ __device__ __forceinline__ void merge_low16(uint32_t *key) {
     }
 }
 
+// kept[0..16) and nk[0..16) sorted -> kept = the 16 smallest of both, sorted (as merge_low16)
+__device__ __forceinline__ void merge_low16_2(uint32_t (&kept)[16], const uint32_t (&nk)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t a = kept[i], b = nk[15 - i];
+        kept[i] = a < b ? a : b;
+    }
+    uint32_t *key = kept;
+#pragma unroll
+    for (int j = 8; j > 0; j >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (!(i & j)) BCHK_CAS(i, i + j)
+    }
+}
+
 // 32-bit sort key: a monotone 26-bit prefix of |y| (5 exponent bits covering
 // [2^-27, 2^5) + 21 mantissa bits) above the 6-bit position. |y| below the range maps to
 // prefix 0 or 1, above it (and inf/NaN) to the all-ones prefix; both are detected after the sort.
@@ -90,22 +106,298 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t hi, uint32_t lo, int pos) 
     return (pre << 6) | (uint32_t)pos;
 }
 
-// Blocks of kFastWaves waves, one 64-codeword chunk per wave: the code tables are staged
-// into LDS once per 512 codewords, and two blocks per CU give 4 waves per SIMD (<= 128
-// VGPRs; the kernel is latency-bound, so occupancy wins).
+// the hard decision yH = (2y/s2 > 0) (:336-342) from the sign bits shifted in from the top
+// (yHl: positions 0..31, yHh: 32..N-1, last position at bit 31)
+template <int N>
+__device__ __forceinline__ uint64_t hard_decision(uint32_t yHl, uint32_t yHh) {
+    if constexpr (N < 32) {
+        yHl >>= 32 - N;
+        yHh = 0;
+    } else if constexpr (N < 64) {
+        yHh >>= 64 - N;
+    }
+    // y > 0 is the clear sign bit: y = +0 (and tiny/subnormal y, whose alpha could
+    // underflow) has prefix 0 and is sent to the slow path by fast_decide
+    return ~(((uint64_t)yHh << 32) | yHl) & ((1ull << N) - 1ull);
+}
+
+// ------------------------------------------------------------------ the per-lane decision
+// What the fast path decides for one codeword (lane), from its 64 sort keys (positions N..63
+// all-ones) and its hard decision yH: returned at i = 0 (state 1) or i = 1 (state 2) with the
+// decoded difference `best` and path metric l0, or unresolved (state 0: the exact kernel
+// decides). bad / ok0 / zero0 classify it for the queue.
+struct FastRes {
+    int state;
+    uint64_t best;
+    double l0;
+    bool bad, ok0, zero0;
+};
+
+// Sort of the 64 keys (positions N..63 all-ones) into the 16 smallest in order, k[0..15].
 // SEL (no per-codeword stats requested, 2 TMAX + 2 <= 16): only the 16 smallest keys are
 // put in order (four sorted groups of 16, then low-half merges) -- the fast-path exits read
 // ranks 0..2t and the least reliable position, so an exact tie beyond rank 2t + 1 cannot
 // change a result, only the BCHK_F_TIE flag of the stats record; SEL = false sorts all 64
-// keys and sends any tie to the exact path, so the flags match it.
+// keys and sends any tie to the exact path, so the flags match it. bad: some |y| outside
+// the keys' range, or (SEL = false) a prefix tie anywhere.
+template <int M, int TMAX, bool SEL>
+__device__ __forceinline__ void fast_sort64(uint32_t (&key)[64], uint32_t &kmax_real, bool &bad) {
+    constexpr int N = Geo<M>::N;
+    kmax_real = 0;  // the largest key of a real position
+    bad = false;
+    if constexpr (SEL) {
+        sort16<0>(key);
+        sort16<16>(key);
+        sort16<32>(key);
+        sort16<48>(key);
+        // padding keys (positions >= N) are all-ones and sort to the top of their group
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int cnt = N - 16 * g < 0 ? 0 : (N - 16 * g > 16 ? 16 : N - 16 * g);
+            if (cnt > 0) kmax_real = key[16 * g + cnt - 1] > kmax_real ? key[16 * g + cnt - 1] : kmax_real;
+        }
+        merge_low16<0, 16>(key);
+        merge_low16<32, 48>(key);
+        merge_low16<0, 32>(key);
+    } else {
+        // ---- bitonic sort of the 64 keys, ascending
+#pragma unroll
+        for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+                for (int i = 0; i < 64; ++i) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const uint32_t a = key[i], b = key[l];
+                        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+                        key[i] = (i & k) ? hi : lo;
+                        key[l] = (i & k) ? lo : hi;
+                    }
+                }
+            }
+        }
+        kmax_real = key[N - 1];
+#pragma unroll
+        for (int r = 0; r < N - 1; ++r) bad |= ((key[r] ^ key[r + 1]) >> 6) == 0u;
+    }
+}
+
+// The decision from the sorted prefix k[0..15] (ranks 0..15 of the 64 keys), the largest
+// real key and the sorter's flags: returned at i = 0 / i = 1, or unresolved.
+template <int M, int TMAX>
+__device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t *lg, const uint32_t *col,
+                                               const uint64_t *chien, const uint32_t *k, uint32_t kmax_real,
+                                               bool bad, uint64_t yH, const double *yrow, bool live, int t,
+                                               double s2) {
+    constexpr int N = Geo<M>::N;
+    constexpr int W = (TMAX + 3) / 4;
+    // calcRightSide takes the first border = 2t+1-m agreeing sorted positions; with m0 == m
+    // (both fast-path exits) and m positions disagreeing, they lie within ranks 0..2t (KMAX).
+    constexpr int KMAX = (2 * TMAX < N - 1) ? 2 * TMAX : N - 1;
+    // (k holds at least ranks 0..KMAX+1: 16 from the selection, 64 from the full sort)
+    // ---- sorted prefix. Distinct 26-bit prefixes imply |y| values >= 2^-21 apart
+    // (relative), so their alphas are strictly ordered exactly as the reference's
+    // (|alpha|, position) order. Any equal prefix sends the codeword to the exact slow
+    // path: beyond rank KMAX+1 the order cannot change this path's result, but an exact
+    // tie anywhere is flagged (BCHK_F_TIE) there, so every path reports the same flags.
+    bad = bad || (k[0] >> 6) <= 1u                       // some |y| < 2^-27 (or zero)
+              || (kmax_real >> 6) == 0x3FFFFFFu;         // some |y| >= 32, inf or NaN
+#pragma unroll
+    for (int r = 0; r < KMAX + 1; ++r) bad |= ((k[r] ^ k[r + 1]) >> 6) == 0u;
+    {   // materialise the flag here, so the sorted keys past the prefix die now
+        uint32_t b = bad ? 1u : 0u;
+        asm volatile("" : "+v"(b));
+        bad = b != 0u;
+    }
+
+    // ---- the sorted prefix calcRightSide can touch: positions packed 5 per word, and a
+    // lower bound of each alpha from its key alone: the prefix is |y| truncated to 21
+    // mantissa bits, so ylo <= |y| < ylo (1 + 2^-20), and lo = ylo * RN(2/s2) lies below
+    // alpha = RN(2|y|/s2) by at most a relative 2^-51. The row is not re-read: the fast
+    // path returns only when l < (sum of lo) (1 - 2^-40) <= calcRightSide(), and queues
+    // every other case (a relative window of 2^-19 more than the exact test) for the
+    // exact kernel. The bounds are formed from the prefix keys where they are summed.
+    constexpr int NPF = KMAX + 1;
+    uint32_t pre[NPF];
+#pragma unroll
+    for (int r = 0; r < NPF; ++r) pre[r] = k[r];
+    const int o0 = (int)(k[0] & 63u);
+    const double c2 = 2.0 / s2;
+    // ---- syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
+    uint32_t S0[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) S0[w] = 0;
+#pragma unroll
+    for (int pos = 0; pos < N; ++pos) {
+        const uint32_t on = ((yH >> pos) & 1ull) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+        for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w] & on;
+    }
+    // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`
+    // (at most t + 1 positions: the error pattern, plus the flipped bit at i = 1).
+    auto accept = [&](uint64_t diff, double &l, bool &ret) {
+        constexpr int LMAX = TMAX + 1;
+        const int m = __popcll(diff);
+        const int border = (2 * t + 1) - m;  // m0 == m on both fast-path exits
+        double g[LMAX];
+        uint64_t v = diff;
+#pragma unroll
+        for (int j = 0; j < LMAX; ++j) {  // independent loads, issued together; only the
+            g[j] = 0.0;                    // flipped positions' (no line fetched for others)
+            if (v) g[j] = yrow[(int)__builtin_ctzll(v)];
+            v &= v - 1;
+        }
+        l = 0.0;
+        v = diff;
+#pragma unroll
+        for (int j = 0; j < LMAX; ++j) {
+            if (v) l += fabs((2.0 * g[j]) / s2);
+            v &= v - 1;
+        }
+        double rs_lo = 0.0;  // lower bound of calcRightSide() (:54-67)
+        int taken = 0;
+#pragma unroll
+        for (int r = 0; r < NPF; ++r) {
+            const bool ag = !((diff >> (pre[r] & 63u)) & 1ull);
+            if (ag && taken < border) {
+                const uint32_t pr = pre[r] >> 6;  // eb (5 bits) | 21 mantissa bits
+                const uint64_t bits = ((uint64_t)((pr >> 21) + (1023u - 27u)) << 52) |
+                                      ((uint64_t)(pr & 0x1FFFFFu) << 31);
+                rs_lo += __longlong_as_double((long long)bits) * c2;
+                ++taken;
+            }
+        }
+        // a certain return only: l < rs_lo (1 - 2^-40) <= rs; the exact path decides the rest
+        ret = (taken >= border) && (l < rs_lo * (1.0 - 0x1p-40));
+    };
+
+    FastRes R;
+    // ---- i = 0 (:361-382)
+    R.state = 0;  // 0 unresolved, 1 returned at i = 0, 2 returned at i = 1
+    R.best = 0;
+    R.l0 = DBL_MAX;
+    Mask<1> E;
+    const bool ok0 = alg_core<M, TMAX>(ex, lg, chien, S0, t, E);
+    if (!bad && ok0) {
+        double l;
+        bool ret;
+        accept(E.w[0], l, ret);
+        if (ret) { R.state = 1; R.best = E.w[0]; R.l0 = l; }
+    }
+    // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371). When the
+    // hard decision is a codeword (zero syndrome, which the decoder rejects), pattern 1 flips
+    // the least reliable position o0 and its syndrome is o0's single column: the decoder
+    // corrects that one error, back to yH, so D = 0 (l = 0) without a decode.
+    bool zero0 = true;
+#pragma unroll
+    for (int w = 0; w < W; ++w) zero0 = zero0 && S0[w] == 0u;
+    if (live && !bad && !ok0 && zero0) {
+        double l;
+        bool ret;
+        accept(0ull, l, ret);
+        if (ret) { R.state = 2; R.best = 0ull; R.l0 = l; }
+    }
+    const bool need1 = live && !bad && !ok0 && !zero0;
+    if (ballot(need1)) {
+        uint32_t S1[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) S1[w] = S0[w] ^ col[o0 * W + w];
+        const bool ok1 = alg_core<M, TMAX>(ex, lg, chien, S1, t, E);
+        if (need1 && ok1) {
+            const uint64_t diff = (1ull << o0) ^ E.w[0];
+            double l;
+            bool ret;
+            accept(diff, l, ret);
+            if (ret) { R.state = 2; R.best = diff; R.l0 = l; }
+        }
+    }
+    R.bad = bad;
+    R.ok0 = ok0;
+    R.zero0 = zero0;
+    return R;
+}
+
+// The fused counters of a wave's 64 codewords (src/dataForPlot.cpp:55-74): e = bit errors of
+// a resolved row (0 otherwise); one reduction per counter, the error ones only when a row has
+// errors (rare: ballot); partial slot by chunk.
+__device__ __forceinline__ void fast_counters(const SearchParams &p, uint32_t cw0, int N, bool resolved, int state,
+                                              uint32_t e) {
+    // per-codeword counts are 0/1 flags times constants: wave sums by ballot popcounts (no
+    // cross-lane reductions); the bit-error sum only when a row has errors (rare)
+    const uint64_t nres = (uint64_t)__popcll(ballot(resolved));
+    const uint64_t nit = (uint64_t)__popcll(ballot(resolved && state == 2));
+    const uint64_t pro = p.variant == BCHK_VARIANT_WORD ? (uint64_t)(2 * N + 1) : 0ull;
+    const uint64_t em = ballot(e != 0u);
+    unsigned long long c[6] = {(unsigned long long)__popcll(em), 0ull, nres + nit,
+                               pro * nres + nit * (uint64_t)(N + 6), pro * nres + nit * (uint64_t)(N + 1), nres};
+    for (uint64_t mm = em; mm; mm &= mm - 1) c[1] += rdl(e, (int)__builtin_ctzll(mm));
+    if ((threadIdx.x & 63) == 0) {
+        unsigned long long *dst6 = p.cnt + (size_t)((cw0 >> 6) % (uint32_t)kCntSlots) * kCntStride;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (c[k]) atomicAdd(dst6 + k, c[k]);
+    }
+}
+
+// l0 and the stats record of a resolved codeword, then every unresolved one into the exact
+// kernel's queue (likely heavy ones -- the hard decision neither decodes nor is a codeword --
+// at the front when the queue is two-ended)
+__device__ __forceinline__ void fast_finish(const SearchParams &p, uint32_t cw, int N, bool live, const FastRes &R) {
+    const bool resolved = live && R.state != 0;
+    if (resolved) {
+        const bool word = p.variant == BCHK_VARIANT_WORD;
+        const uint64_t pro = word ? (uint64_t)(2 * N + 1) : 0ull;
+        const uint64_t iters = R.state == 2 ? 1ull : 0ull;
+        if (p.l0) p.l0[cw] = R.l0;
+        if (p.st) {
+            bchk_stats st;
+            st.decodes = iters + 1;
+            st.comparisons = pro + iters * (uint64_t)(N + 6);
+            st.sums = pro + iters * (uint64_t)(N + 1);
+            st.iterations = iters;
+            st.jsteps = 0;
+            st.improvements = 0;
+            st.flags = BCHK_F_ACCEPTED | BCHK_F_RETURNED;
+            st.reserved = 0;
+            p.st[cw] = st;
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    const bool unres = live && R.state == 0;
+    const uint64_t um = ballot(unres);
+    if (um && p.qfront) {
+        const bool hv = unres && !R.bad && !R.ok0 && !R.zero0;
+        const uint64_t hm = ballot(hv), om = um & ~hm;
+        const uint64_t below = (1ull << lane) - 1ull;
+        uint32_t bf = 0, bb = 0;
+        if (lane == 0) {
+            if (hm) bf = atomicAdd(p.qfront, (uint32_t)__popcll(hm));
+            if (om) bb = atomicAdd(p.qback, (uint32_t)__popcll(om));
+            atomicAdd(p.qtail, (uint32_t)__popcll(um));
+        }
+        bf = (uint32_t)__shfl((int)bf, 0, 64);
+        bb = (uint32_t)__shfl((int)bb, 0, 64);
+        if (hv) p.queue_out[bf + (uint32_t)__popcll(hm & below)] = cw;
+        else if (unres) p.queue_out[p.count - 1u - (bb + (uint32_t)__popcll(om & below))] = cw;
+    } else if (um) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(p.qtail, (uint32_t)__popcll(um));
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        if (unres) p.queue_out[base + (uint32_t)__popcll(um & ((1ull << lane) - 1ull))] = cw;
+    }
+}
+
+// ------------------------------------------------------------ staged kernel (BCHK_FAST_RING=0)
+// Blocks of kFastWaves waves, one 64-codeword chunk per wave: the code tables are staged
+// into LDS once per 512 codewords, and two blocks per CU give 4 waves per SIMD (<= 128
+// VGPRs). Each wave stages its rows through LDS in 8-position slices (coalesced 8-B loads
+// via registers).
 template <int M, int TMAX, bool SEL>
 __global__ void __launch_bounds__(kWaveSize * kFastWaves, 4)
 kaneko_fast_kernel(SearchParams p) {
     constexpr int N = Geo<M>::N;
     static_assert(N <= 63, "fast path covers n <= 63");
-    constexpr int W = (TMAX + 3) / 4;
-    // calcRightSide takes the first border = 2t+1-m agreeing sorted positions; with m0 == m
-    // (both fast-path exits) and m positions disagreeing, they lie within ranks 0..2t (KMAX).
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
     __syncthreads();
@@ -117,32 +409,11 @@ kaneko_fast_kernel(SearchParams p) {
     double *stage = reinterpret_cast<double *>(smem + ((p.td.bytes + 15) & ~15u) + wid * kStageBytes);
     const uint32_t cw0 = (blockIdx.x * kFastWaves + wid) * 64u;
     if (cw0 >= p.count) return;
-    // experiment (BCHK_FAST_STAGGER): the first round's second block on each CU starts
-    // p.fast_stagger cycles late, so the CU's two blocks load and compute out of phase
-    if (p.fast_stagger && blockIdx.x >= p.fast_blocks / 2 && blockIdx.x < p.fast_blocks) {
-        const uint64_t t0 = __builtin_amdgcn_s_memtime();
-        while (__builtin_amdgcn_s_memtime() - t0 < p.fast_stagger) __builtin_amdgcn_s_sleep(8);
-    }
     const uint32_t cw = cw0 + (uint32_t)lane;
     const bool live = cw < p.count;
-    const int t = p.t;
-    (void)M;
-    const double s2 = p.s2;
     const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
     static_assert(64 * N + 256 <= kStageBytes, "output block and row errors fit the stage");
 
-#ifdef BCHK_DIAG
-    // stamps: [0] stage+keys, [1] sort, [2] S0, [3] decode i=0 + accept, [4] i=1, [5] outputs
-    unsigned long long dg[6], tp = __builtin_amdgcn_s_memtime();
-#define BCHK_STAMP(i)                                          \
-    {                                                          \
-        const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
-        dg[i] = tn - tp;                                       \
-        tp = tn;                                               \
-    }
-#else
-#define BCHK_STAMP(i)
-#endif
     // ---- stage rows, build keys and the hard decision yH = (2y/s2 > 0) (:336-342).
     // Slice loads run kAhead slices ahead of the slice being turned into keys, so a wave
     // waits for one memory round trip instead of one per slice.
@@ -191,220 +462,20 @@ kaneko_fast_kernel(SearchParams p) {
     }
 #pragma unroll
     for (int q = N; q < 64; ++q) key[q] = 0xFFFFFFFFu;
-    // yHl/yHh hold the sign bits of positions 0..31 / 32..N-1, last position at bit 31
-    if constexpr (N < 32) {
-        yHl >>= 32 - N;
-        yHh = 0;
-    } else if constexpr (N < 64) {
-        yHh >>= 64 - N;
-    }
-    const uint64_t yH = ~(((uint64_t)yHh << 32) | yHl) & ((1ull << N) - 1ull);
-    BCHK_STAMP(0)
-#if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 1
-    if (p.l0 && live) p.l0[cw] = (double)(key[5] ^ key[17] ^ key[40] ^ (uint32_t)yH);
-    return;
-#endif
+    const uint64_t yH = hard_decision<N>(yHl, yHh);
+    uint32_t kmax_real;
+    bool bad;
+    fast_sort64<M, TMAX, SEL>(key, kmax_real, bad);
+    const FastRes R = fast_decide<M, TMAX>(ex, lg, col, chien, key, kmax_real, bad, yH, yrow, live, p.t, p.s2);
 
-    constexpr int KMAX = (2 * TMAX < N - 1) ? 2 * TMAX : N - 1;
-    static_assert(!SEL || KMAX + 2 <= 16, "selection keeps 16 ranks");
-    uint32_t kmax_real = 0;  // the largest key of a real position (SEL)
-    if constexpr (SEL) {
-        // ---- the 16 smallest keys in order: four sorted groups, low halves merged
-        sort16<0>(key);
-        sort16<16>(key);
-        sort16<32>(key);
-        sort16<48>(key);
-        // padding keys (positions >= N) are all-ones and sort to the top of their group
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int cnt = N - 16 * g < 0 ? 0 : (N - 16 * g > 16 ? 16 : N - 16 * g);
-            if (cnt > 0) kmax_real = key[16 * g + cnt - 1] > kmax_real ? key[16 * g + cnt - 1] : kmax_real;
-        }
-        merge_low16<0, 16>(key);
-        merge_low16<32, 48>(key);
-        merge_low16<0, 32>(key);
-    } else {
-        // ---- bitonic sort of the 64 keys, ascending
-#pragma unroll
-        for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-            for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-                for (int i = 0; i < 64; ++i) {
-                    const int l = i ^ j;
-                    if (l > i) {
-                        const uint32_t a = key[i], b = key[l];
-                        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-                        key[i] = (i & k) ? hi : lo;
-                        key[l] = (i & k) ? lo : hi;
-                    }
-                }
-            }
-        }
-        kmax_real = key[N - 1];
-    }
-
-    BCHK_STAMP(1)
-#if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 2
-    if (p.l0 && live) p.l0[cw] = (double)(key[5] ^ key[17] ^ key[40] ^ (uint32_t)yH);
-    return;
-#endif
-    // ---- sorted prefix. Distinct 26-bit prefixes imply |y| values >= 2^-21 apart
-    // (relative), so their alphas are strictly ordered exactly as the reference's
-    // (|alpha|, position) order. Any equal prefix sends the codeword to the exact slow
-    // path: beyond rank KMAX+1 the order cannot change this path's result, but an exact
-    // tie anywhere is flagged (BCHK_F_TIE) there, so every path reports the same flags.
-    bool bad = (key[0] >> 6) <= 1u                       // some |y| < 2^-27 (or zero)
-               || (kmax_real >> 6) == 0x3FFFFFFu;        // some |y| >= 32, inf or NaN
-    constexpr int NTIE = SEL ? KMAX + 1 : N - 1;         // adjacent pairs checked for ties
-#pragma unroll
-    for (int r = 0; r < NTIE; ++r) bad |= ((key[r] ^ key[r + 1]) >> 6) == 0u;
-    {   // materialise the flag here, so the sorted keys past the prefix die now
-        uint32_t b = bad ? 1u : 0u;
-        asm volatile("" : "+v"(b));
-        bad = b != 0u;
-    }
-
-    // ---- the sorted prefix calcRightSide can touch: positions packed 5 per word, and a
-    // lower bound of each alpha from its key alone: the prefix is |y| truncated to 21
-    // mantissa bits, so ylo <= |y| < ylo (1 + 2^-20), and lo = ylo * RN(2/s2) lies below
-    // alpha = RN(2|y|/s2) by at most a relative 2^-51. The row is not re-read: the fast
-    // path returns only when l < (sum of lo) (1 - 2^-40) <= calcRightSide(), and queues
-    // every other case (a relative window of 2^-19 more than the exact test) for the
-    // exact kernel.
-    constexpr int NPF = KMAX + 1;
-    constexpr int NPW = (NPF + 4) / 5;
-    uint32_t ppk[NPW];
-#pragma unroll
-    for (int w = 0; w < NPW; ++w) ppk[w] = 0;
-#pragma unroll
-    for (int r = 0; r < NPF; ++r) ppk[r / 5] |= (key[r] & 63u) << (6 * (r % 5));
-    auto ppos = [&](int r) { return (int)((ppk[r / 5] >> (6 * (r % 5))) & 63u); };
-    const int o0 = (int)(key[0] & 63u);
-    double alo[NPF];
-    {
-        const double c2 = 2.0 / s2;
-#pragma unroll
-        for (int r = 0; r < NPF; ++r) {
-            const uint32_t pre = key[r] >> 6;  // eb (5 bits) | 21 mantissa bits
-            const uint64_t bits = ((uint64_t)((pre >> 21) + (1023u - 27u)) << 52) |
-                                  ((uint64_t)(pre & 0x1FFFFFu) << 31);
-            alo[r] = __longlong_as_double((long long)bits) * c2;
-        }
-    }
-    // ---- syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
-    uint32_t S0[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) S0[w] = 0;
-#pragma unroll
-    for (int pos = 0; pos < N; ++pos) {
-        const uint32_t on = ((yH >> pos) & 1ull) ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-        for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w] & on;
-    }
-
-    BCHK_STAMP(2)
-#if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 3
-    if (p.l0 && live) p.l0[cw] = (double)(alo[0] + alo[NPF - 1] + (double)(S0[0] ^ ppk[0] ^ (uint32_t)bad));
-    return;
-#endif
-    // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`
-    // (at most t + 1 positions: the error pattern, plus the flipped bit at i = 1).
-    auto accept = [&](uint64_t diff, double &l, bool &ret) {
-        constexpr int LMAX = TMAX + 1;
-        const int m = __popcll(diff);
-        const int border = (2 * t + 1) - m;  // m0 == m on both fast-path exits
-        double g[LMAX];
-        uint64_t v = diff;
-#pragma unroll
-        for (int j = 0; j < LMAX; ++j) {  // independent loads, issued together; only the
-            g[j] = 0.0;                    // flipped positions' (no line fetched for others)
-            if (v) g[j] = yrow[(int)__builtin_ctzll(v)];
-            v &= v - 1;
-        }
-        l = 0.0;
-        v = diff;
-#pragma unroll
-        for (int j = 0; j < LMAX; ++j) {
-            if (v) l += fabs((2.0 * g[j]) / s2);
-            v &= v - 1;
-        }
-        double rs_lo = 0.0;  // lower bound of calcRightSide() (:54-67)
-        int taken = 0;
-#pragma unroll
-        for (int r = 0; r < NPF; ++r) {
-            const bool ag = !((diff >> ppos(r)) & 1ull);
-            if (ag && taken < border) {
-                rs_lo += alo[r];
-                ++taken;
-            }
-        }
-        // a certain return only: l < rs_lo (1 - 2^-40) <= rs; the exact path decides the rest
-        ret = (taken >= border) && (l < rs_lo * (1.0 - 0x1p-40));
-    };
-
-    // ---- i = 0 (:361-382)
-    int state = 0;  // 0 unresolved, 1 returned at i = 0, 2 returned at i = 1
-    uint64_t best = 0;
-    double l0 = DBL_MAX;
-    Mask<1> E;
-#ifdef BCHK_FAST_VALU  // experiment: Berlekamp-Massey on the VALU (spread GF products)
-    const bool ok0 = alg_core_valu<M, TMAX>(chien, S0, t, E);
-#else
-    const bool ok0 = alg_core<M, TMAX>(ex, lg, chien, S0, t, E);
-#endif
-    if (!bad && ok0) {
-        double l;
-        bool ret;
-        accept(E.w[0], l, ret);
-        if (ret) { state = 1; best = E.w[0]; l0 = l; }
-    }
-    BCHK_STAMP(3)
-#if defined(BCHK_FAST_CUT) && BCHK_FAST_CUT == 4
-    if (p.l0 && live) p.l0[cw] = (double)(l0 + (double)(state ^ (uint32_t)best));
-    return;
-#endif
-    // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371). When the
-    // hard decision is a codeword (zero syndrome, which the decoder rejects), pattern 1 flips
-    // the least reliable position o0 and its syndrome is o0's single column: the decoder
-    // corrects that one error, back to yH, so D = 0 (l = 0) without a decode.
-    bool zero0 = true;
-#pragma unroll
-    for (int w = 0; w < W; ++w) zero0 = zero0 && S0[w] == 0u;
-    if (live && !bad && !ok0 && zero0) {
-        double l;
-        bool ret;
-        accept(0ull, l, ret);
-        if (ret) { state = 2; best = 0ull; l0 = l; }
-    }
-    const bool need1 = live && !bad && !ok0 && !zero0;
-    if (ballot(need1)) {
-        uint32_t S1[W];
-#pragma unroll
-        for (int w = 0; w < W; ++w) S1[w] = S0[w] ^ col[o0 * W + w];
-#ifdef BCHK_FAST_VALU
-        const bool ok1 = alg_core_valu<M, TMAX>(chien, S1, t, E);
-#else
-        const bool ok1 = alg_core<M, TMAX>(ex, lg, chien, S1, t, E);
-#endif
-        if (need1 && ok1) {
-            const uint64_t diff = (1ull << o0) ^ E.w[0];
-            double l;
-            bool ret;
-            accept(diff, l, ret);
-            if (ret) { state = 2; best = diff; l0 = l; }
-        }
-    }
-
-    BCHK_STAMP(4)
     // ---- outputs: resolved rows through LDS, one coalesced 64-row block per wave. The
     // unresolved rows of the block are read back and written unchanged (the exact kernel,
     // which runs after this one on the same stream, then owns them): measured against
     // writing only the resolved rows (16-B chunks that also touch an unresolved row stored
     // byte by byte) the read-back is 8 % faster at 5 dB -- 84 % of waves hold an unresolved row
-    const bool resolved = live && state != 0;
+    const bool resolved = live && R.state != 0;
     uint8_t *out = reinterpret_cast<uint8_t *>(stage);
-    const uint64_t x = yH ^ best;
+    const uint64_t x = yH ^ R.best;
     if (resolved) {
 #pragma unroll
         for (int pos = 0; pos < N; ++pos) out[lane * N + pos] = (uint8_t)((x >> pos) & 1ull);
@@ -422,8 +493,8 @@ kaneko_fast_kernel(SearchParams p) {
         for (int i = lane; i < rows * N; i += 64) dst[i] = out[i];
     }
     if (p.cnt) {
-        // fused counters (src/dataForPlot.cpp:55-74) of the resolved rows: the sent words'
-        // block against the output block, 16 B at a time; differing bytes are rare
+        // fused counters of the resolved rows: the sent words' block against the output
+        // block, 16 B at a time; differing bytes are rare
         uint32_t *rowerr = reinterpret_cast<uint32_t *>(out + 64 * N);
         rowerr[lane] = 0u;
         wave_sync();
@@ -448,74 +519,289 @@ kaneko_fast_kernel(SearchParams p) {
                 if (txb[i] != out[i]) atomicAdd(&rowerr[i / N], 1u);
         }
         wave_sync();
-        const uint32_t e = resolved ? rowerr[lane] : 0u;
-        const uint64_t it = state == 2 ? 1ull : 0ull;
-        const uint64_t pro = p.variant == BCHK_VARIANT_WORD ? (uint64_t)(2 * N + 1) : 0ull;
-        unsigned long long c[6] = {e ? 1ull : 0ull, e, resolved ? it + 1 : 0ull,
-                                   resolved ? pro + it * (uint64_t)(N + 6) : 0ull,
-                                   resolved ? pro + it * (uint64_t)(N + 1) : 0ull, resolved ? 1ull : 0ull};
-        // frame / bit errors are rare: a ballot decides whether they need a reduction
-        const bool anyerr = ballot(e != 0u) != 0ull;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            if (k < 2 && !anyerr) continue;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) c[k] += (unsigned long long)__shfl_xor((long long)c[k], o, 64);
-        }
-        if (lane == 0) {
-            unsigned long long *dst6 = p.cnt + (size_t)((cw0 >> 6) % (uint32_t)kCntSlots) * kCntStride;
-#pragma unroll
-            for (int k = 0; k < 6; ++k)
-                if (c[k]) atomicAdd(dst6 + k, c[k]);
-        }
+        fast_counters(p, cw0, N, resolved, R.state, resolved ? rowerr[lane] : 0u);
     }
-    if (resolved) {
-        const bool word = p.variant == BCHK_VARIANT_WORD;
-        const uint64_t pro = word ? (uint64_t)(2 * N + 1) : 0ull;
-        const uint64_t iters = state == 2 ? 1ull : 0ull;
-        if (p.l0) p.l0[cw] = l0;
-        if (p.st) {
-            bchk_stats st;
-            st.decodes = iters + 1;
-            st.comparisons = pro + iters * (uint64_t)(N + 6);
-            st.sums = pro + iters * (uint64_t)(N + 1);
-            st.iterations = iters;
-            st.jsteps = 0;
-            st.improvements = 0;
-            st.flags = BCHK_F_ACCEPTED | BCHK_F_RETURNED;
-            st.reserved = 0;
-            p.st[cw] = st;
-        }
-    }
-    BCHK_STAMP(5)
-#ifdef BCHK_DIAG
-    if (p.diag && lane == 0)
-        for (int q = 0; q < 6; ++q) p.diag[(size_t)(cw0 / 64) * 8 + q] = dg[q];
+    fast_finish(p, cw, N, live, R);
+}
+
+// ------------------------------------------------------------------ ring kernel (default)
+// Workgroups of kRingWaves waves, kRingPerCU per CU, persistent over the batch's 64-codeword
+// chunks (chunk b, b + G, b + 2G, ... for workgroup b of G). Wave 0 is the loader: it copies each chunk's
+// rows -- 64 x n contiguous f64, exactly the caller's layout -- from HBM into a ring of LDS
+// slots with gfx950 direct-to-LDS loads (global_load_lds_dwordx4: no VGPRs, one 1-KiB
+// wave-instruction per 1 KiB, every line read once, fully coalesced), up to two chunks in
+// flight, and publishes a slot once its loads have landed (a counted vmcnt wait, then the
+// slot's tag in LDS). The other waves compute: each claims the workgroup's next chunk, reads its
+// 64 rows from the slot (lane r reads row r: row stride 8n bytes keeps ds_read_b64
+// conflict-free), turns them into sort keys -- selecting the 16 smallest on the way, 32 keys
+// held at a time -- and gives the slot back, then runs the same decision as the staged kernel
+// (fast_decide). Selection only (no stats record: the staged kernel serves those calls). So the chip streams the next chunks while it
+// computes the current ones, instead of every wave loading, then computing, in step with
+// the others. Outputs leave without an LDS row image: each lane's decoded word is one 64-bit
+// mask, and the block's 16-B pieces are expanded from the masks (the caller's bytes kept
+// for unresolved rows, which are not written) and stored coalesced.
+#ifndef BCHK_FAST_RING_SLOTS
+#define BCHK_FAST_RING_SLOTS 2
 #endif
-#undef BCHK_STAMP
-    // ---- everything else goes to the exact wave-per-codeword path
-    const bool unres = live && state == 0;
-    const uint64_t um = ballot(unres);
-    if (um && p.qfront) {
-        // likely heavy: the hard decision itself does not decode (nor is it a codeword)
-        const bool hv = unres && !bad && !ok0 && !zero0;
-        const uint64_t hm = ballot(hv), om = um & ~hm;
-        const uint64_t below = (1ull << lane) - 1ull;
-        uint32_t bf = 0, bb = 0;
-        if (lane == 0) {
-            if (hm) bf = atomicAdd(p.qfront, (uint32_t)__popcll(hm));
-            if (om) bb = atomicAdd(p.qback, (uint32_t)__popcll(om));
-            atomicAdd(p.qtail, (uint32_t)__popcll(um));
+#ifndef BCHK_FAST_RING_WAVES
+#define BCHK_FAST_RING_WAVES 12
+#endif
+#ifndef BCHK_FAST_RING_PER_CU
+#define BCHK_FAST_RING_PER_CU 2
+#endif
+constexpr int kRingSlots = BCHK_FAST_RING_SLOTS;
+constexpr int kRingWaves = BCHK_FAST_RING_WAVES;  // 1 loader + the compute waves
+constexpr int kRingPerCU = BCHK_FAST_RING_PER_CU; // workgroups per CU (LDS and VGPRs sized for it)
+constexpr int kRingWPE = (kRingWaves * kRingPerCU + 3) / 4;  // waves per SIMD
+constexpr int kRingWaveBytes = 64 * 8 + 64 * 4;  // decoded masks + row error counts
+struct RingCtl {
+    uint32_t tag[kRingSlots];  // chunk + 1 once the slot holds that chunk's rows, 0 = free
+    uint32_t claim;            // next chunk for a compute wave
+    uint32_t pad[3];
+};
+template <int M>
+constexpr size_t ring_slot_bytes() { return (size_t)64 * Geo<M>::N * 8; }
+template <int M>
+constexpr size_t ring_lds_bytes(size_t tables) {
+    return ((tables + 15) & ~size_t(15)) + kRingSlots * ring_slot_bytes<M>() + sizeof(RingCtl) +
+           (kRingWaves - 1) * kRingWaveBytes;
+}
+
+__device__ __forceinline__ void glds16(const void *src, uint8_t *lds_dst) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds_dst, 16, 0, 0);
+}
+__device__ __forceinline__ uint32_t lds_ld32(const uint32_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st32(uint32_t *a, uint32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+constexpr uint32_t kRingSpin = 1u << 24;  // bounded waits: a guard against logic errors
+constexpr uint32_t kFaultFastRing = 32u;
+
+// 4 bits -> 4 bytes of 0/1 (bit k to byte k)
+__device__ __forceinline__ uint32_t nib_bytes(uint32_t nib) { return (nib * 0x00204081u) & 0x01010101u; }
+
+template <int M, int TMAX>
+__global__ void __launch_bounds__(kWaveSize * kRingWaves) __attribute__((amdgpu_waves_per_eu(kRingWPE, kRingWPE)))
+kaneko_fast_ring_kernel(SearchParams p) {
+    constexpr int N = Geo<M>::N;
+    static_assert(N <= 63, "fast path covers n <= 63");
+    constexpr int KMAX = (2 * TMAX < N - 1) ? 2 * TMAX : N - 1;
+    static_assert(KMAX + 2 <= 16, "the 16-key selection covers the decision's ranks");
+    constexpr uint32_t SLOT = (uint32_t)ring_slot_bytes<M>();
+    static_assert(SLOT % 512 == 0, "a slot is whole half-instructions of 16-B pieces");
+    constexpr int NG = (int)((SLOT + 1023) / 1024);  // glds wave-instructions per chunk
+    static_assert(NG <= 32, "two chunks in flight fit the vmcnt field");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    load_tables(smem, p.tables, p.td.bytes);
+    uint8_t *ring = smem + ((p.td.bytes + 15) & ~15u);
+    RingCtl *ctl = reinterpret_cast<RingCtl *>(ring + kRingSlots * SLOT);
+    if (threadIdx.x < sizeof(RingCtl) / 4) reinterpret_cast<uint32_t *>(ctl)[threadIdx.x] = 0u;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = uni((int)(threadIdx.x >> 6));  // wave-uniform: SGPRs
+    const uint32_t nch = (p.count + 63u) / 64u, nfull = p.count / 64u;
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t K = b < nch ? (nch - b + G - 1u) / G : 0u;  // this workgroup's chunks
+
+    if (wid == 0) {
+        // ------------------------------------------------------------------ loader
+        uint32_t issued = 0, published = 0, spins = 0;
+        while (published < K) {
+            while (issued < K && issued - published < 2u) {
+                const uint32_t s = issued % kRingSlots;
+                if (lds_ld32(&ctl->tag[s]) != 0u) break;  // still held by a compute wave
+                const uint32_t gk = b + issued * G;
+                if (gk < nfull && p.fast_mode != 1u) {  // a partial last chunk: read by its compute wave
+                    const uint8_t *src = reinterpret_cast<const uint8_t *>(p.y) + (size_t)gk * SLOT + 16u * lane;
+                    uint8_t *dst = ring + s * SLOT;
+#pragma unroll
+                    for (int i = 0; i < NG; ++i)
+                        if (1024u * i + 16u * lane < SLOT) glds16(src + 1024u * i, dst + 1024u * i);
+                }
+                ++issued;
+            }
+            if (issued == published) {  // no slot free yet
+                if (++spins > kRingSpin) {
+                    if (lane == 0 && p.fault) atomicOr(p.fault, kFaultFastRing);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            spins = 0;
+            // the oldest chunk in flight has landed once at most the newer one's loads remain
+            const bool newer = issued - published == 2u && b + (published + 1u) * G < nfull;
+            if (newer) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NG) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (lane == 0) lds_st32(&ctl->tag[published % kRingSlots], published + 1u);
+            ++published;
         }
-        bf = (uint32_t)__shfl((int)bf, 0, 64);
-        bb = (uint32_t)__shfl((int)bb, 0, 64);
-        if (hv) p.queue_out[bf + (uint32_t)__popcll(hm & below)] = cw;
-        else if (unres) p.queue_out[p.count - 1u - (bb + (uint32_t)__popcll(om & below))] = cw;
-    } else if (um) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(p.qtail, (uint32_t)__popcll(um));
-        base = (uint32_t)__shfl((int)base, 0, 64);
-        if (unres) p.queue_out[base + (uint32_t)__popcll(um & ((1ull << lane) - 1ull))] = cw;
+        return;
+    }
+    // ---------------------------------------------------------------------- compute
+    const uint8_t *ex = smem + p.td.off_exp;
+    const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
+    const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
+    const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
+    uint8_t *wb = reinterpret_cast<uint8_t *>(ctl + 1) + (wid - 1) * kRingWaveBytes;
+    uint64_t *xm = reinterpret_cast<uint64_t *>(wb);
+    uint32_t *rowerr = reinterpret_cast<uint32_t *>(wb + 64 * 8);
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&ctl->claim, 1u);
+        k = (uint32_t)uni((int)__shfl((int)k, 0, 64));
+        if (k >= K) break;
+        const uint32_t gk = b + k * G, cw0 = 64u * gk;
+        const uint32_t cw = cw0 + (uint32_t)lane;
+        const bool live = cw < p.count;
+        const bool full = gk < nfull;
+        const uint32_t s = k % kRingSlots;
+        {   // the slot: published by the loader
+            uint32_t sp = 0;
+            while (lds_ld32(&ctl->tag[s]) != k + 1u && ++sp < kRingSpin) __builtin_amdgcn_s_sleep(1);
+            if (sp >= kRingSpin) {
+                if (lane == 0 && p.fault) atomicOr(p.fault, kFaultFastRing);
+                break;
+            }
+        }
+        // ---- keys and the hard decision yH = (2y/s2 > 0) (:336-342) from the rows, 16
+        // positions at a time: each group of 16 keys is sorted (Green's network) and merged
+        // into the 16 smallest so far, so only 32 keys are ever held (registers for more
+        // waves per SIMD); the same selection as fast_sort64's
+        uint32_t kept[16];
+        uint32_t kmax_real = 0, yHl = 0, yHh = 0;
+        auto build = [&](auto rd) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                uint32_t nk[16];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {  // 8 reads in flight at a time
+                    double v8[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int pos = 16 * g + 8 * h + i;
+                        if (pos < N) v8[i] = rd(pos);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int pos = 16 * g + 8 * h + i;
+                        if (pos < N) {
+                            const uint64_t bb = (uint64_t)__double_as_longlong(v8[i]);
+                            const uint32_t hi = (uint32_t)(bb >> 32), lo = (uint32_t)bb;
+                            nk[8 * h + i] = sort_key(hi, lo, pos);
+                            if (pos < 32) yHl = (yHl >> 1) | (hi & 0x80000000u);
+                            else yHh = (yHh >> 1) | (hi & 0x80000000u);
+                        } else {
+                            nk[8 * h + i] = 0xFFFFFFFFu;
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                sort16<0>(nk);
+                const int cnt = N - 16 * g < 0 ? 0 : (N - 16 * g > 16 ? 16 : N - 16 * g);
+                if (cnt > 0) kmax_real = nk[cnt - 1] > kmax_real ? nk[cnt - 1] : kmax_real;
+                if (g == 0) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) kept[i] = nk[i];
+                } else {
+                    merge_low16_2(kept, nk);
+                }
+            }
+        };
+        if (full) {  // the slot (LDS)
+            typedef __attribute__((address_space(3))) const double *LdsF64;
+            LdsF64 row = (LdsF64)(ring + s * SLOT);  // a C cast: generic -> LDS address space
+            row += lane * N;
+            build([&](int pos) { return row[pos]; });
+        } else {     // the partial last chunk, from HBM
+            const double *row = p.y + (size_t)(live ? cw : cw0) * N;
+            build([&](int pos) { return row[pos]; });
+        }
+        // every read of the slot has returned (its values are in the keys): give it back
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wave_sync();
+        if (lane == 0) lds_st32(&ctl->tag[s], 0u);
+        const uint64_t yH = hard_decision<N>(yHl, yHh);
+        if (p.fast_mode == 2u) {  // experiment: the rows' path alone (wrong results)
+            if (p.l0 && live) p.l0[cw] = (double)(kept[3] ^ kmax_real ^ (uint32_t)yH);
+            continue;
+        }
+        const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
+        // t and s2 re-read opaquely per chunk: nothing derived from them is hoisted out of
+        // the persistent loop (it would stay live through the selection and spill)
+        int t = p.t;
+        double s2 = p.s2;
+        asm volatile("" : "+s"(t), "+s"(s2));
+        const FastRes R = fast_decide<M, TMAX>(ex, lg, col, chien, kept, kmax_real, false, yH, yrow, live, t, s2);
+
+        // ---- outputs
+        const bool resolved = live && R.state != 0;
+        const uint64_t x = yH ^ R.best;
+        uint32_t e = 0;
+        uint8_t *dst = p.res + (size_t)cw0 * N;
+        const uint8_t *txb = p.tx ? p.tx + (size_t)cw0 * N : nullptr;
+        if (N >= 16 && full && ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(txb)) & 15u) == 0) {
+            // the block's 4n 16-B pieces from the 64 masks: piece q holds bytes 16q .. 16q + 15
+            // = positions o .. of row r1 = 16q / n (and the first ones of row r1 + 1: n >= 16)
+            const uint64_t rm = ballot(resolved);
+            xm[lane] = x;
+            rowerr[lane] = 0u;
+            wave_sync();
+            bool anyerr = false;
+            for (int q = lane; q < 4 * N; q += 64) {
+                const int b0 = 16 * q, r1 = b0 / N, o = b0 - N * r1;
+                const bool span = o > N - 16;  // the piece reaches row r1 + 1
+                const int r2 = span ? r1 + 1 : r1;
+                const uint64_t x1 = xm[r1], x2 = xm[r2];
+                const uint64_t w = (x1 >> o) | (span ? x2 << (N - o) : 0ull);
+                uint32_t nw[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) nw[d] = nib_bytes((uint32_t)(w >> (4 * d)) & 15u);
+                // bytes of unresolved rows are not written (the exact kernel owns them, and
+                // may run concurrently on another XCD: no stale byte may be stored over its
+                // result); a piece shared with one goes out byte by byte (rare)
+                const uint32_t in2 = span ? (0xFFFFu << (N - o)) & 0xFFFFu : 0u;  // bytes of r2
+                const uint32_t keep = (((rm >> r1) & 1ull) ? 0u : (~in2 & 0xFFFFu)) |
+                                      (((rm >> r2) & 1ull) ? 0u : in2);
+                if (!keep) {
+                    reinterpret_cast<uint4 *>(dst)[q] = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+                } else if (keep != 0xFFFFu) {
+                    for (uint32_t wm = ~keep & 0xFFFFu; wm; wm &= wm - 1) {
+                        const int i = __builtin_ctz(wm);
+                        dst[16 * q + i] = (uint8_t)(nw[i >> 2] >> (8 * (i & 3)));
+                    }
+                }
+                if (txb) {  // fused counters: bytes that differ from the sent word (rare)
+                    const uint4 a = reinterpret_cast<const uint4 *>(txb)[q];
+                    const uint32_t xx[4] = {a.x ^ nw[0], a.y ^ nw[1], a.z ^ nw[2], a.w ^ nw[3]};
+                    if (xx[0] | xx[1] | xx[2] | xx[3]) {
+                        anyerr = true;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i)
+                            if ((xx[i >> 2] >> (8 * (i & 3))) & 0xFFu) atomicAdd(&rowerr[i < N - o ? r1 : r2], 1u);
+                    }
+                }
+            }
+            if (txb) {
+                if (ballot(anyerr)) {
+                    wave_sync();
+                    e = resolved ? rowerr[lane] : 0u;
+                }
+            }
+        } else if (resolved) {  // partial chunk (or unaligned buffers): the row byte by byte
+            for (int pos = 0; pos < N; ++pos) {
+                const uint8_t bit = (uint8_t)((x >> pos) & 1ull);
+                dst[lane * N + pos] = bit;
+                if (txb) e += txb[lane * N + pos] != bit ? 1u : 0u;
+            }
+        }
+        if (p.cnt) fast_counters(p, cw0, N, resolved, R.state, e);
+        fast_finish(p, cw, N, live, R);
+        wave_sync();  // xm / rowerr are rewritten by the next chunk
     }
 }
 
@@ -531,13 +817,53 @@ static hipError_t launch_fast_sel(const SearchParams &p, size_t lds, hipStream_t
     return hipGetLastError();
 }
 
+// the ring kernel: one workgroup per CU (persistent), LDS sized by ring_lds_bytes
+static int device_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+template <int M, int TMAX>
+static hipError_t launch_fast_ring(const SearchParams &p, hipStream_t s) {
+    const uint32_t chunks = (p.count + 63u) / 64u;
+    const int blocks = (int)std::min<uint32_t>(chunks, (uint32_t)(kRingPerCU * device_cus()));
+    const size_t lds = ring_lds_bytes<M>(p.td.bytes);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)&kaneko_fast_ring_kernel<M, TMAX>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    const int waves = p.fast_waves ? std::min((int)p.fast_waves, kRingWaves) : kRingWaves;
+    hipLaunchKernelGGL((kaneko_fast_ring_kernel<M, TMAX>), dim3(blocks), dim3(kWaveSize * waves), lds, s, p);
+    return hipGetLastError();
+}
+
+// BCHK_FAST_RING=0 in the environment selects the staged kernel (measurements)
+static bool use_ring() {
+    static int r = -1;
+    if (r < 0) {
+        const char *e = getenv("BCHK_FAST_RING");
+        r = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return r != 0;
+}
+
 template <int M, int TMAX>
 static hipError_t launch_fast_impl(const SearchParams &p, size_t lds, hipStream_t s) {
     constexpr int N = Geo<M>::N;
     constexpr int KMAX = (2 * TMAX < N - 1) ? 2 * TMAX : N - 1;
     if constexpr (KMAX + 2 <= 16) {
         // no stats record: the flags are not observable, selection suffices
-        if (!p.st && !getenv("BCHK_FAST_FULLSORT")) return launch_fast_sel<M, TMAX, true>(p, lds, s);
+        if (!p.st && !getenv("BCHK_FAST_FULLSORT")) {
+            const bool ring = use_ring() && kRingPerCU * ring_lds_bytes<M>(p.td.bytes) <= 160 * 1024;
+            return ring ? launch_fast_ring<M, TMAX>(p, s) : launch_fast_sel<M, TMAX, true>(p, lds, s);
+        }
     }
     return launch_fast_sel<M, TMAX, false>(p, lds, s);
 }

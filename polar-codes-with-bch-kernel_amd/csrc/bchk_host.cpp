@@ -432,9 +432,9 @@ struct bchk_ctx {
     // idle waves of the tail kernel help a sibling's split codeword decode its exact chunks
     // (BCHK_AN_HELP=0: off; results identical either way)
     bool an_help = true;
-    // lane fast kernel, experiment: the first round's second block per CU starts
-    // BCHK_FAST_STAGGER cycles late (fast_blocks = the first round's blocks)
-    uint32_t fast_blocks = 0, fast_stagger = 0;
+    // fast ring kernel: waves per workgroup (BCHK_FAST_RING_WAVES, 0 = 16) and experiment
+    // mode (BCHK_FAST_MODE)
+    uint32_t fast_waves = 0, fast_mode = 0;
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
     // hybrid tail: a first-pass hand-off whose loop bound is below this goes to a cooperative
@@ -648,8 +648,8 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             f.qback = ctrl + kQBack;
         }
         if (c->m <= 6) {
-            f.fast_blocks = c->fast_blocks;
-            f.fast_stagger = c->fast_stagger;
+            f.fast_waves = c->fast_waves;
+            f.fast_mode = c->fast_mode;
         }
         HIP_TRY(c->fast(f, c->lds_fast, s));
     }
@@ -883,10 +883,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (const char *tc = getenv("BCHK_TAIL_CONCURRENT")) c->tail_concurrent = atoi(tc) != 0;
     if (const char *ti = getenv("BCHK_TAIL_INLINE")) c->tail_inline = atoi(ti) != 0;
     if (const char *ah = getenv("BCHK_AN_HELP")) c->an_help = atoi(ah) != 0;
-    if (const char *fs = getenv("BCHK_FAST_STAGGER")) {
-        c->fast_stagger = (uint32_t)std::max(0, atoi(fs));
-        c->fast_blocks = 2u * (uint32_t)prop.multiProcessorCount;  // the first round's blocks
-    }
+    if (const char *fw = getenv("BCHK_FAST_RING_WAVES")) c->fast_waves = (uint32_t)std::max(2, std::min(16, atoi(fw)));
+    if (const char *fm = getenv("BCHK_FAST_MODE")) c->fast_mode = (uint32_t)std::max(0, atoi(fm));
     if (const char *tb = getenv("BCHK_TAIL_BLOCKS")) c->tail_conc_blocks = std::max(1, atoi(tb));
     if (const char *tm = getenv("BCHK_TAIL_MIN_BOUND")) c->tail_min_bound = strtoull(tm, nullptr, 10);
     if (const char *hf = getenv("BCHK_HEAVY_FIRST")) c->heavy_first = atoi(hf) != 0;
