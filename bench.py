@@ -284,7 +284,10 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
     # select_fast); without it stage 0 is only the control-block memset
     # (n > 63: kaneko_first_kernel, the first test patterns of every codeword)
     has_fast = args.m >= 7 or args.t <= {3: 3, 4: 7, 5: 8, 6: 6}.get(args.m, -1)
-    fast_name = "kaneko_fast_kernel" if args.m <= 6 else "kaneko_first_kernel"
+    # n <= 63: the ring kernel serves calls without a stats record where the 16-key selection
+    # covers the decision (csrc/bchk_fast.hip launch_fast_impl), else the staged kernel
+    ring = (min(2 * tm, n - 1) + 2 <= 16 and not args.unfused and os.environ.get("BCHK_FAST_RING", "1") != "0")
+    fast_name = ("kaneko_fast_ring_kernel" if ring else "kaneko_fast_kernel") if args.m <= 6 else "kaneko_first_kernel"
     fast_on = has_fast and ms4[0] > 0 and n_exact < B
     # per launch: average duration (HIP events on the launching stream) and the codewords
     # one launch processes

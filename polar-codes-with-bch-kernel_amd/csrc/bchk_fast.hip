@@ -540,14 +540,18 @@ kaneko_fast_kernel(SearchParams p) {
 // the others. Outputs leave without an LDS row image: each lane's decoded word is one 64-bit
 // mask, and the block's 16-B pieces are expanded from the masks (the caller's bytes kept
 // for unresolved rows, which are not written) and stored coalesced.
+// default: one 16-wave workgroup per CU with 4 slots (147 KB of LDS at n = 63). Measured at
+// 5 dB / 6 dB (fast kernel alone, profiles/r05_fast/): 16 waves / 4 slots 0.233-0.235 /
+// 0.163 ms, 2 x 12 waves / 2 slots 0.241 / 0.177, 2 x 10 waves 0.238 / 0.213, staged
+// kernel 0.237 / 0.190
 #ifndef BCHK_FAST_RING_SLOTS
-#define BCHK_FAST_RING_SLOTS 2
+#define BCHK_FAST_RING_SLOTS 4
 #endif
 #ifndef BCHK_FAST_RING_WAVES
-#define BCHK_FAST_RING_WAVES 12
+#define BCHK_FAST_RING_WAVES 16
 #endif
 #ifndef BCHK_FAST_RING_PER_CU
-#define BCHK_FAST_RING_PER_CU 2
+#define BCHK_FAST_RING_PER_CU 1
 #endif
 constexpr int kRingSlots = BCHK_FAST_RING_SLOTS;
 constexpr int kRingWaves = BCHK_FAST_RING_WAVES;  // 1 loader + the compute waves
