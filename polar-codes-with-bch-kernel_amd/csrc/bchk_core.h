@@ -140,6 +140,73 @@ __device__ __forceinline__ uint32_t gf_exp2(const uint8_t *ex, int la, int lb) {
     else return ex[s < ZL ? s : ZL];
 }
 
+// GF(2^m) table views for the per-lane decoders (bm_locator, split_test, alg_decode_lanes).
+// A view hands out log "handles" and forms products from two of them; the arithmetic the
+// decoders need on logs (division, doubling, the log(0) sentinel) goes through it.
+//   GfPlain: the packed tables (exp u8 with 4n entries for m >= 7, log u16): handle = log.
+//   GfRep (m >= 7, bchk_kernels.hip's cooperative kernel): the same tables replicated 16
+//     times with one 4-B entry per replica, entry e of replica r at byte 64 e + 4 r, lanes
+//     reading replica lane & 15 -- a 32-lane LDS group then touches each bank at most twice
+//     (lanes l and l + 16), against ~3.5 distinct dwords per bank for random byte lookups
+//     into the packed table (the cooperative kernel's LDS array was 88 % busy, half of it
+//     in bank conflicts, r05 PMC). handle = 64 log + 4 r, so a product is one
+//     v_add3 (a + b - 4 r) and one ds_read_b32, as before one add and one ds_read_u8.
+template <int M>
+struct GfPlain {
+    static constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL;
+    const uint8_t *ex;
+    const uint16_t *lg_;
+    __device__ __forceinline__ int lg(uint32_t g) const { return lg_[g]; }
+    __device__ __forceinline__ uint32_t mul(int a, int b) const { return gf_exp2<M>(ex, a, b); }
+    __device__ __forceinline__ int zl() const { return ZL; }
+    __device__ __forceinline__ int one() const { return 0; }
+    __device__ __forceinline__ bool is_zl(int h) const { return h == ZL; }
+    // log(x / y) for x, y != 0
+    __device__ __forceinline__ int div(int a, int b) const { const int d = a - b; return d < 0 ? d + N : d; }
+    // log(x^2) for x != 0
+    __device__ __forceinline__ int dbl(int h) const { const int s2 = 2 * h; return s2 >= N ? s2 - N : s2; }
+    __device__ __forceinline__ int plain(int h) const { return h; }  // the packed table's log
+};
+constexpr int kGfRepStride = 64;   // bytes per entry (16 replicas x 4 B)
+template <int M>
+constexpr int gf_rep_exp_entries() { return 4 * Geo<M>::N; }  // the 4n-entry exp table (m >= 7)
+template <int M>
+constexpr int gf_rep_bytes() { return (gf_rep_exp_entries<M>() + (1 << M)) * kGfRepStride; }
+template <int M>
+struct GfRep {
+    static constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL, S = kGfRepStride;
+    const uint8_t *rep;  // LDS: exp entries 0 .. 4n-1, then log entries 0 .. 2^m - 1
+    int lo;              // 4 (lane & 15)
+    __device__ __forceinline__ int lg(uint32_t g) const {
+        return *reinterpret_cast<const int *>(rep + (gf_rep_exp_entries<M>() + (int)g) * S + lo);
+    }
+    __device__ __forceinline__ uint32_t mul(int a, int b) const {
+        return *reinterpret_cast<const uint32_t *>(rep + (a + b - lo));
+    }
+    __device__ __forceinline__ int zl() const { return ZL * S + lo; }
+    __device__ __forceinline__ int one() const { return lo; }
+    __device__ __forceinline__ bool is_zl(int h) const { return h == ZL * S + lo; }
+    __device__ __forceinline__ int div(int a, int b) const {
+        const int d = a - b;
+        return (d < 0 ? d + N * S : d) + lo;
+    }
+    __device__ __forceinline__ int dbl(int h) const {
+        const int s2 = 2 * h - lo;
+        return s2 >= N * S + lo ? s2 - N * S : s2;
+    }
+    __device__ __forceinline__ int plain(int h) const { return (h - lo) / S; }
+};
+// fills the replicated tables from the packed ones (a whole workgroup, before a barrier)
+template <int M>
+__device__ __forceinline__ void gf_rep_fill(uint8_t *rep, const uint8_t *ex, const uint16_t *lg) {
+    constexpr int NE = gf_rep_exp_entries<M>(), NL = 1 << M;
+    for (int i = threadIdx.x; i < (NE + NL) * 16; i += blockDim.x) {
+        const int e = i >> 4, r = i & 15;
+        const uint32_t v = e < NE ? (uint32_t)ex[e] : (uint32_t)(lg[e - NE] * kGfRepStride + 4 * r);
+        *reinterpret_cast<uint32_t *>(rep + i * 4) = v;
+    }
+}
+
 template <int NW>
 __device__ __forceinline__ void mask_set(Mask<NW> &m, int p) {
 #pragma unroll
@@ -165,64 +232,64 @@ __device__ __forceinline__ int mask_popc(const Mask<NW> &m) {
 // coefficient; the inversionless form (gamma C + d x B, two products) gives the same C up to
 // a nonzero scalar at every step (by induction: its C, B and gamma are this form's times
 // the same running product of discrepancies), so the same L, degree and roots.
-template <int M, int TMAX>
-__device__ __forceinline__ void bm_locator(const uint8_t *__restrict__ ex,
-                                           const uint16_t *__restrict__ lg, const uint32_t *Sw,
-                                           int t, uint32_t (&C)[TMAX + 1], int &Lout) {
-    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL;
+template <int M, int TMAX, class GF>
+__device__ __forceinline__ void bm_locator_g(const GF &gf, const uint32_t *Sw, int t, uint32_t (&C)[TMAX + 1],
+                                             int &Lout) {
     int lS[2 * TMAX];  // lS[j-1] = log S_j
 #pragma unroll
-    for (int j = 0; j < TMAX; ++j) lS[2 * j] = lg[(Sw[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+    for (int j = 0; j < TMAX; ++j) lS[2 * j] = gf.lg((Sw[j >> 2] >> (8 * (j & 3))) & 0xFFu);
 #pragma unroll
     for (int e = 2; e <= 2 * TMAX - 1; e += 2) {  // S_{2i} = S_i^2
         const int h = lS[e / 2 - 1];
-        int sq = 2 * h;
-        sq = sq >= N ? sq - N : sq;
-        lS[e - 1] = (h == ZL) ? ZL : sq;
+        lS[e - 1] = gf.is_zl(h) ? h : gf.dbl(h);
     }
     // binary Berlekamp-Massey over S_1, S_3, ... (even steps vanish)
     int lB[TMAX + 1];
 #pragma unroll
-    for (int i = 0; i <= TMAX; ++i) { C[i] = i ? 0u : 1u; lB[i] = i ? ZL : 0; }
-    int lb = 0, L = 0;
+    for (int i = 0; i <= TMAX; ++i) { C[i] = i ? 0u : 1u; lB[i] = i ? gf.zl() : gf.one(); }
+    int lb = gf.one(), L = 0;
 #pragma unroll
     for (int k = 0; k < TMAX; ++k) {
         if (k < t) {
             const int r = 2 * k;
             int lC[TMAX + 1];
 #pragma unroll
-            for (int i = 0; i <= TMAX; ++i) lC[i] = lg[C[i]];
+            for (int i = 0; i <= TMAX; ++i) lC[i] = gf.lg(C[i]);
             // before step k, deg C <= L <= 2k-1; after it, deg C <= 2k+1 (terms beyond are
             // zero whenever the final L <= t, the only case that can succeed)
             uint32_t d = 0;
 #pragma unroll
             for (int i = 0; i <= (2 * k - 1 > 0 ? (2 * k - 1 < TMAX ? 2 * k - 1 : TMAX) : 0); ++i)
-                d ^= gf_exp2<M>(ex, lC[i], lS[r - i]);
-            const int ld = lg[d];
+                d ^= gf.mul(lC[i], lS[r - i]);
+            const int ld = gf.lg(d);
             const bool chg = (d != 0u) && (2 * L <= r);
-            int lf = ld - lb;  // log(d / b); d = 0 leaves C as it is
-            lf = lf < 0 ? lf + N : lf;
-            lf = d ? lf : ZL;
+            const int lf = d ? gf.div(ld, lb) : gf.zl();  // log(d / b); d = 0 leaves C as it is
 #pragma unroll
             for (int i = TMAX; i >= 1; --i) {
                 if (i > 2 * k + 1) { C[i] = 0u; continue; }
-                C[i] ^= gf_exp2<M>(ex, lf, lB[i - 1]);
+                C[i] ^= gf.mul(lf, lB[i - 1]);
             }
             // B <- C_old (length change) or x*B; then x*B for the skipped odd step
 #pragma unroll
             for (int i = TMAX; i >= 0; --i) {
-                const int shifted1 = i ? lB[i - 1] : ZL;
+                const int shifted1 = i ? lB[i - 1] : gf.zl();
                 const int next = chg ? lC[i] : shifted1;
                 lB[i] = next;
             }
 #pragma unroll
             for (int i = TMAX; i >= 1; --i) lB[i] = lB[i - 1];
-            lB[0] = ZL;
+            lB[0] = gf.zl();
             L = chg ? r + 1 - L : L;
             lb = chg ? ld : lb;
         }
     }
     Lout = L;
+}
+template <int M, int TMAX>
+__device__ __forceinline__ void bm_locator(const uint8_t *__restrict__ ex,
+                                           const uint16_t *__restrict__ lg, const uint32_t *Sw,
+                                           int t, uint32_t (&C)[TMAX + 1], int &Lout) {
+    bm_locator_g<M, TMAX>(GfPlain<M>{ex, lg}, Sw, t, C, Lout);
 }
 
 template <int M, int TMAX>
@@ -462,30 +529,28 @@ __device__ __forceinline__ bool alg_core_valu(const uint64_t *__restrict__ chien
 // experiment, and the GPU parity tests through the exhaustive/random decoder tables).
 //
 // x g mod rho-hat (rho / C_0, monic: x^TMAX = sum_j q_j x^j), g linear, lq = log q
-template <int M, int TMAX>
-__device__ __forceinline__ void mulx_mod(const uint8_t *__restrict__ ex, const uint16_t *__restrict__ lg,
-                                         const int (&lq)[TMAX], uint32_t (&g)[TMAX]) {
-    const int lt = lg[g[TMAX - 1]];
+template <int M, int TMAX, class GF>
+__device__ __forceinline__ void mulx_mod(const GF &gf, const int (&lq)[TMAX], uint32_t (&g)[TMAX]) {
+    const int lt = gf.lg(g[TMAX - 1]);
 #pragma unroll
-    for (int j = TMAX - 1; j >= 0; --j) g[j] = (j ? g[j - 1] : 0u) ^ gf_exp2<M>(ex, lt, lq[j]);
+    for (int j = TMAX - 1; j >= 0; --j) g[j] = (j ? g[j - 1] : 0u) ^ gf.mul(lt, lq[j]);
 }
 // g^2 mod rho-hat: squares of the coefficients (Frobenius), then the top-down reduction of
 // degrees 2 TMAX - 2 .. TMAX
-template <int M, int TMAX>
-__device__ __forceinline__ void sqr_mod(const uint8_t *__restrict__ ex, const uint16_t *__restrict__ lg,
-                                        const int (&lq)[TMAX], uint32_t (&g)[TMAX]) {
+template <int M, int TMAX, class GF>
+__device__ __forceinline__ void sqr_mod(const GF &gf, const int (&lq)[TMAX], uint32_t (&g)[TMAX]) {
     uint32_t sq[2 * TMAX - 1];
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) {
-        const int l = lg[g[j]];
-        sq[2 * j] = gf_exp2<M>(ex, l, l);
+        const int l = gf.lg(g[j]);
+        sq[2 * j] = gf.mul(l, l);
         if (j + 1 < TMAX) sq[2 * j + 1] = 0u;
     }
 #pragma unroll
     for (int k = 2 * TMAX - 2; k >= TMAX; --k) {
-        const int lk = lg[sq[k]];
+        const int lk = gf.lg(sq[k]);
 #pragma unroll
-        for (int j = 0; j < TMAX; ++j) sq[k - TMAX + j] ^= gf_exp2<M>(ex, lk, lq[j]);
+        for (int j = 0; j < TMAX; ++j) sq[k - TMAX + j] ^= gf.mul(lk, lq[j]);
     }
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) g[j] = sq[j];
@@ -495,18 +560,14 @@ constexpr int ilog2c(int v) { return v < 2 ? 0 : 1 + ilog2c(v / 2); }
 
 // lambda = C (logs lc), deg >= 1, C_0 != 0: true iff lambda has deg distinct roots in GF(2^m)*
 // (lanes with act = false give an unspecified answer)
-template <int M, int TMAX>
-__device__ __forceinline__ bool split_test(const uint8_t *__restrict__ ex, const uint16_t *__restrict__ lg,
-                                           const int (&lc)[TMAX + 1], int deg, bool act) {
-    constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL;
+template <int M, int TMAX, class GF>
+__device__ __forceinline__ bool split_test(const GF &gf, const int (&lc)[TMAX + 1], int deg, bool act) {
     static_assert(TMAX >= 2, "split test needs TMAX >= 2");
     int lq[TMAX];
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) {  // q_j = C_(TMAX - j) / C_0
         const int v = lc[TMAX - j];
-        int d = v - lc[0];
-        d = d < 0 ? d + N : d;
-        lq[j] = v == ZL ? ZL : d;
+        lq[j] = gf.is_zl(v) ? v : gf.div(v, lc[0]);
     }
     // x^(2P) for the largest power of two P <= TMAX - 1 (so 2P >= TMAX): x^TMAX = q, then
     // 2P - TMAX multiplications by x; then squarings up to x^(2^m)
@@ -515,18 +576,18 @@ __device__ __forceinline__ bool split_test(const uint8_t *__restrict__ ex, const
     static_assert(SQ >= 1, "2P < 2^m");
     uint32_t g[TMAX];
 #pragma unroll
-    for (int j = 0; j < TMAX; ++j) g[j] = gf_exp2<M>(ex, lq[j], 0);
+    for (int j = 0; j < TMAX; ++j) g[j] = gf.mul(lq[j], gf.one());
 #pragma unroll
-    for (int e = TMAX; e < 2 * P; ++e) mulx_mod<M, TMAX>(ex, lg, lq, g);
+    for (int e = TMAX; e < 2 * P; ++e) mulx_mod<M, TMAX>(gf, lq, g);
 #pragma unroll
-    for (int s = 0; s < SQ; ++s) sqr_mod<M, TMAX>(ex, lg, lq, g);
+    for (int s = 0; s < SQ; ++s) sqr_mod<M, TMAX>(gf, lq, g);
     // times x^s, s = TMAX - deg (per lane; the wave runs the largest s of its active lanes)
     const int sh = (act && deg >= 2) ? TMAX - deg : 0;
     for (int st = 0; ballot(st < sh); ++st) {
         uint32_t h[TMAX];
 #pragma unroll
         for (int j = 0; j < TMAX; ++j) h[j] = g[j];
-        mulx_mod<M, TMAX>(ex, lg, lq, h);
+        mulx_mod<M, TMAX>(gf, lq, h);
 #pragma unroll
         for (int j = 0; j < TMAX; ++j) g[j] = st < sh ? h[j] : g[j];
     }
@@ -542,27 +603,29 @@ __device__ __forceinline__ bool split_test(const uint8_t *__restrict__ ex, const
 // positions l + 64 s, as alg_decode_wave), one scan per successful lane. Same decision and
 // flipped positions as alg_core. Lanes with act = false report failure without the tests
 // (the caller knows their outcome cannot matter).
-template <int M, int TMAX>
-__device__ __forceinline__ bool alg_decode_lanes(const uint8_t *__restrict__ ex,
-                                                 const uint16_t *__restrict__ lg, const uint32_t *Sw,
-                                                 int t, Mask<Geo<M>::NW> &E, bool act = true) {
+template <int M, int TMAX, class GF>
+__device__ __forceinline__ bool alg_decode_lanes_g(const GF &gf, const uint8_t *__restrict__ ex, const uint32_t *Sw,
+                                                   int t, Mask<Geo<M>::NW> &E, bool act = true) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
     const int lane = (int)__lane_id();
     uint32_t C[TMAX + 1];
     int L;
-    bm_locator<M, TMAX>(ex, lg, Sw, t, C, L);
+    bm_locator_g<M, TMAX>(gf, Sw, t, C, L);
     int deg = 0;
 #pragma unroll
     for (int i = 1; i <= TMAX; ++i) deg = C[i] ? i : deg;
     int lc[TMAX + 1];
 #pragma unroll
-    for (int i = 0; i <= TMAX; ++i) lc[i] = lg[C[i]];
+    for (int i = 0; i <= TMAX; ++i) lc[i] = gf.lg(C[i]);
     bool ok = act && (L <= t) && (deg >= 1);
 #if defined(BCHK_SPLIT_CUT)  // experiment builds only (wrong results): Berlekamp-Massey alone
     ok = ok && lc[0] == 12345;
 #else
-    if (ballot(ok)) ok = split_test<M, TMAX>(ex, lg, lc, deg, ok) && ok;
+    if (ballot(ok)) ok = split_test<M, TMAX>(gf, lc, deg, ok) && ok;
 #endif
+    // the Chien scan below reads the packed exp table with plain logs
+#pragma unroll
+    for (int i = 0; i <= TMAX; ++i) lc[i] = gf.plain(lc[i]);
 #pragma unroll
     for (int s = 0; s < NW; ++s) E.w[s] = 0;
     for (uint64_t sm = ballot(ok); sm; sm &= sm - 1) {
@@ -599,6 +662,13 @@ __device__ __forceinline__ bool alg_decode_lanes(const uint8_t *__restrict__ ex,
         if (lane == src && cnt != dg) ok = false;  // never: the split test said deg roots
     }
     return ok;
+}
+
+template <int M, int TMAX>
+__device__ __forceinline__ bool alg_decode_lanes(const uint8_t *__restrict__ ex,
+                                                 const uint16_t *__restrict__ lg, const uint32_t *Sw,
+                                                 int t, Mask<Geo<M>::NW> &E, bool act = true) {
+    return alg_decode_lanes_g<M, TMAX>(GfPlain<M>{ex, lg}, ex, Sw, t, E, act);
 }
 
 // The decoder a kernel uses: VALU BM for m <= 6 unless BCHK_GF_LDS is defined; m >= 7 the

@@ -908,10 +908,10 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
         }
         return per_cu * prop.multiProcessorCount;
     };
-    c->grid_coop = grid_of(c->ks.coop_ptr(), kCoopThreads, c->lds_coop);
+    c->grid_coop = grid_of(c->ks.coop_ptr(), c->ks.coop_threads, c->lds_coop);
     c->grid = grid_of(c->ks.search_ptr(), kWaveSize * kWavesPerBlock, c->lds);
     if (c->ks.search_tab) {
-        c->grid_coop_tab = grid_of(c->ks.coop_tab_ptr(), kCoopThreads, c->lds_coop);
+        c->grid_coop_tab = grid_of(c->ks.coop_tab_ptr(), c->ks.coop_threads, c->lds_coop);
         c->grid_tab = grid_of(c->ks.search_tab_ptr(), kWaveSize * kWavesPerBlock, c->lds_tab);
     }
     if (c->ks.tail) c->grid_tail = grid_of(c->ks.tail_ptr(), kWaveSize * kWavesPerBlock, c->lds_tail);

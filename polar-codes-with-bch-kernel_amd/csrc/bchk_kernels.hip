@@ -431,7 +431,19 @@ constexpr int kLongRec = 2;
 template <int NW>
 constexpr int coop_slots() { return NW == 1 ? BCHK_COOP_SLOTS : kLongSlots; }
 static_assert(BCHK_COOP_SLOTS <= 64, "ring flags are polled one slot per lane");
-static_assert(kLongSlots <= kCoopSlotsMax && kLongSlots >= (kCoopWaves - 1) * kLongClaim + 8,
+// m >= 7: waves of the cooperative workgroup (1 acceptor + decoders). 12 waves = 3 per SIMD
+// leave each wave 168 VGPRs, which the packed decoder (Berlekamp-Massey and the split test
+// per lane) needs without spilling; at 16 waves (128 VGPRs) it spilled 184-332 B per lane.
+#ifndef BCHK_LONG_COOP_WAVES
+#define BCHK_LONG_COOP_WAVES 12
+#endif
+// the packed decoders' GF tables: 1 = replicated (GfRep, bank-spread), 0 = the packed tables
+#ifndef BCHK_LONG_GFREP
+#define BCHK_LONG_GFREP 0
+#endif
+template <int M>
+constexpr int coop_waves() { return Geo<M>::NW > 1 ? BCHK_LONG_COOP_WAVES : kCoopWaves; }
+static_assert(kLongSlots <= kCoopSlotsMax && kLongSlots >= (BCHK_LONG_COOP_WAVES - 1) * kLongClaim + 8,
               "every decoder's claim fits");
 
 template <int NW>
@@ -466,6 +478,20 @@ template <int NW>
 constexpr size_t coop_ring_bytes() {
     return NW == 1 ? sizeof(CoopSlot<NW>) * coop_slots<NW>()
                    : sizeof(LongSlot<NW>) * kLongSlots + ((sizeof(LongDense<NW>) + 15) & ~size_t(15));
+}
+
+// the cooperative kernel's per-wave LDS: n <= 63 one prep slice per wave; m >= 7 ONE prep
+// slice (every wave builds the same prep, so all of them write the same values), a 128-B
+// scratch per wave (long_decode_claim's chunk masks and syndromes), then the replicated GF
+// tables of the packed decoders (GfRep)
+constexpr int kCoopScratch = 128;  // 8 G + 4 G W bytes (G = kLongClaim, W <= 8)
+template <int M, int TMAX>
+struct PrepTab;
+template <int M, int TMAX>
+constexpr size_t coop_wave_area() {
+    return Geo<M>::NW == 1 ? (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES
+                           : (size_t)Smem<M, TMAX>::WAVE_BYTES + (size_t)coop_waves<M>() * kCoopScratch +
+                                 (BCHK_LONG_GFREP ? (size_t)gf_rep_bytes<M>() : 0) + sizeof(PrepTab<M, TMAX>);
 }
 
 struct CoopCtl {
@@ -555,23 +581,59 @@ __device__ __forceinline__ void mask_flip(Mask<NW> &m, int p) {
     for (int s = 0; s < NW; ++s) m.w[s] ^= (uint64_t)((p >> 6) == s) << (p & 63);
 }
 
-// A decoder wave's claim of nch <= kLongClaim chunks c .. c + nch - 1 (m >= 7): the
-// patterns skip_lane leaves, packed 64 per round (the k-th of them in lane k), decoded; each
-// success goes, in pattern order, into its chunk's success mask and -- when it is a strict
-// running minimum of l below l0 as published (the candidates of the dense ring) -- into the
-// chunk's slot. Chunks at or past the published bound are marked, not decoded; chunks past
-// the cap are not published.
+// The prep's test-pattern tables in the workgroup's LDS (m >= 7, written once per codeword by
+// the acceptor wave): the decoder waves read them there instead of holding the Prep fields in
+// registers and moving them between lanes (readlane / ds_bpermute). Round 4's attempt to
+// serve dense re-decodes through the claim's own call site decoded BCH(127, t = 10) words
+// wrongly: lanes read P.Lo values of other lanes as 0 or as another lane's value
+// (gpurun_out/diag_m7dbg.log) -- cross-lane reads of register-resident prep fields in a kernel
+// that spilled 58-90 VGPRs; with the tables here no decoder reads another lane's register.
 template <int M, int TMAX>
-__device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_t c, uint64_t capc, uint64_t bnd,
-                                                  double l0r, uint64_t skey, int t, const uint8_t *ex,
-                                                  const uint16_t *lg, const uint64_t *chien, const double *ap,
-                                                  void *wscratch, LongSlot<Geo<M>::NW> *ring, CoopCtl *ctl,
-                                                  int lane, uint32_t nch, int lrec) {
+struct PrepTab {
+    static constexpr int W = Prep<M, TMAX>::W, NW = Geo<M>::NW;
+    uint32_t scol[64 * W];  // rank b: odd-syndrome column of position ord[b] (b < NB)
+    uint32_t Lo[64 * W];    // pattern bits 0..5 = l: their syndrome contribution
+    uint64_t Plo[64 * NW];  // pattern bits 0..5 = l: their flipped positions
+    uint32_t S0[W];         // odd syndromes of the hard decision
+};
+template <int M, int TMAX>
+__device__ __forceinline__ void prep_tab_store(PrepTab<M, TMAX> *pt, const Prep<M, TMAX> &P, int lane) {
+    constexpr int W = Prep<M, TMAX>::W, NW = Geo<M>::NW;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        pt->scol[lane * W + w] = P.scol[w];
+        pt->Lo[lane * W + w] = P.Lo[w];
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < NW; ++s2) pt->Plo[lane * NW + s2] = P.Plo.w[s2];
+    if (lane < W) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) v = lane == w ? P.S0[w] : v;
+        pt->S0[lane] = v;
+    }
+}
+
+// A decoder wave's work (m >= 7), one call site for both kinds:
+//  * a claim of nch <= kLongClaim chunks c .. c + nch - 1: the patterns skip_lane leaves,
+//    packed 64 per round (the k-th of them in lane k), decoded; each success goes, in pattern
+//    order, into its chunk's success mask and -- when it is a strict running minimum of l
+//    below l0 as published (the candidates of the dense ring) -- into the chunk's slot.
+//    Chunks past the cap are not published.
+//  * dense (the acceptor's request for a chunk with more candidates than its slot keeps):
+//    every pattern of chunk c, lane = pattern, every lane's result into the dense buffer.
+template <int M, int TMAX, class GF>
+__device__ __forceinline__ int long_decode(const PrepTab<M, TMAX> *pt, const uint8_t *ordl, uint32_t c, uint64_t capc,
+                                           double l0r, uint64_t skey, int t, const uint8_t *ex,
+                                           const GF &gfr, const double *ap, uint8_t *wscratch,
+                                           LongSlot<Geo<M>::NW> *ring, LongDense<Geo<M>::NW> *dn, CoopCtl *ctl,
+                                           int lane, uint32_t nch, int lrec, bool dense) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW, W = Prep<M, TMAX>::W, G = kLongClaim;
     constexpr int NB = N < 31 ? N : 31;
     static_assert(G <= 64 && (G & (G - 1)) == 0, "lanes 0..G-1 form the claim's chunk syndromes");
-    // per-wave LDS scratch (the wave's sorted-|alpha| slice, used by the acceptor only):
-    // the chunks' pattern masks and the syndromes of the hard decision ^ pattern bits >= 6
+    static_assert(8 * G + 4 * G * W <= kCoopScratch, "the wave's scratch holds the claim's masks and syndromes");
+    // per-wave LDS scratch: the chunks' pattern masks and the syndromes of the hard decision
+    // ^ pattern bits >= 6
     uint64_t *actl = reinterpret_cast<uint64_t *>(wscratch);
     uint32_t *hl = reinterpret_cast<uint32_t *>(actl + G);
     int pre[G + 1];
@@ -580,10 +642,11 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
     for (int g = 0; g < G; ++g) {
         const uint64_t b = 64ull * (uint64_t)(c + (uint32_t)g);
         const bool own = (uint32_t)g < nch;  // chunks past nch belong to later claims
-        const uint64_t a = (own && b < capc && b < bnd) ? ballot(!skip_lane(skey, b + (uint64_t)lane, t)) : 0ull;
+        uint64_t a = (!dense && own && b < capc) ? ballot(!skip_lane(skey, b + (uint64_t)lane, t)) : 0ull;
+        a = (dense && g == 0) ? ~0ull : a;
         if (lane == 0) actl[g] = a;
         pre[g + 1] = pre[g] + __popcll(a);
-        if (own && b < capc && lane == 0) {  // the slot's running state (the ring space is ours)
+        if (!dense && own && b < capc && lane == 0) {  // the slot's running state (the ring space is ours)
             LongSlot<NW> &S = ring[(c + (uint32_t)g) % kLongSlots];
             S.okm = 0ull;
             S.ncand = 0u;
@@ -593,12 +656,12 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
     {   // lane g < G: the syndrome of pattern bits >= 6 for chunk c + g
         uint32_t h[W];
 #pragma unroll
-        for (int w = 0; w < W; ++w) h[w] = P.S0[w];
+        for (int w = 0; w < W; ++w) h[w] = pt->S0[w];
         const uint32_t hb = (c + (uint32_t)(lane & (G - 1))) << 6;
         for (int b = 6; b < NB; ++b) {
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-                const uint32_t col_b = rdl(P.scol[w], b);
+                const uint32_t col_b = pt->scol[b * W + w];  // a broadcast read, then the select
                 h[w] ^= ((hb >> b) & 1u) ? col_b : 0u;
             }
         }
@@ -621,25 +684,31 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
         const int bit = valid ? select_bit(actl[g], idx - pg) : 0;
         uint32_t Sw[W];
 #pragma unroll
-        for (int w = 0; w < W; ++w) Sw[w] = hl[g * W + w] ^ (uint32_t)__shfl((int)P.Lo[w], bit, 64);
+        for (int w = 0; w < W; ++w) Sw[w] = hl[g * W + w] ^ pt->Lo[bit * W + w];
         Mask<NW> E;
-        const bool ok = alg_decode_word<M, TMAX>(ex, lg, chien, Sw, t, E, valid) && valid;
+        const bool ok = alg_decode_lanes_g<M, TMAX>(gfr, ex, Sw, t, E, valid) && valid;
         const uint64_t okb = ballot(ok);
-        if (!okb) continue;
-        // the successes (rare): diff = flipped positions ^ error locations, m, calcL (:69-77)
+        if (!okb && !dense) continue;
+        // the successes: diff = flipped positions ^ error locations, m, calcL (:69-77)
         const uint32_t ii = 64u * (c + (uint32_t)g) + (uint32_t)bit;
         Mask<NW> d = E;
         double l = 0.0;
         int m = 0;
         if (ok) {
-            for (int b = 0; b < NB; ++b) {
-                const int pb = (int)rdl((uint32_t)P.ordb, b);
-                if ((ii >> b) & 1u) mask_flip<NW>(d, pb);
-            }
+            for (int b = 0; b < NB; ++b)
+                if ((ii >> b) & 1u) mask_flip<NW>(d, (int)ordl[b]);
             m = mask_popc<NW>(d);
 #pragma unroll
             for (int s2 = 0; s2 < NW; ++s2)
                 for (uint64_t v = d.w[s2]; v; v &= v - 1) l += ap[64 * s2 + (int)__builtin_ctzll(v)];
+        }
+        if (dense) {  // lane = pattern: every lane's result (the acceptor reads okm's lanes)
+#pragma unroll
+            for (int s2 = 0; s2 < NW; ++s2) dn->diff[lane * NW + s2] = d.w[s2];
+            dn->l[lane] = l;
+            dn->m[lane] = (uint32_t)m;
+            if (lane == 0) dn->okm = okb;
+            continue;
         }
         for (uint64_t sm = okb; sm; sm &= sm - 1) {  // pattern order (lane order in a round)
             const int L = (int)__builtin_ctzll(sm);
@@ -668,50 +737,20 @@ __device__ __forceinline__ int long_decode_claim(const Prep<M, TMAX> &P, uint32_
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (!dense) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint32_t cg = c + (uint32_t)g;
-        if ((uint32_t)g >= nch || 64ull * cg >= capc) break;  // not ours / never read by the acceptor
-        if (lane == 0) lds_st(&ctl->ready[cg % kLongSlots], cg + 1u);
+        for (int g = 0; g < G; ++g) {
+            const uint32_t cg = c + (uint32_t)g;
+            if ((uint32_t)g >= nch || 64ull * cg >= capc) break;  // not ours / never read by the acceptor
+            if (lane == 0) lds_st(&ctl->ready[cg % kLongSlots], cg + 1u);
+        }
     }
     wave_sync();
     return (A + 63) >> 6;  // decode rounds
 }
 
-// A decoder wave serves a pending dense request (the acceptor's, for an overflowing chunk):
-// every lane's result of the chunk into the dense buffer. true if it served one.
-template <int M, int TMAX>
-__device__ __forceinline__ bool long_serve_redo(const Prep<M, TMAX> &P, const SearchParams &p, CoopCtl *ctl,
-                                                LongDense<Geo<M>::NW> *dn, const uint8_t *ex,
-                                                const uint16_t *lg, const uint64_t *chien, const double *ap,
-                                                int lane) {
-    constexpr int NW = Geo<M>::NW;
-    uint32_t r = 0;
-    if (lane == 0) {
-        r = lds_ld(&ctl->redo);
-        if (r && atomicCAS(&ctl->redo, r, 0u) != r) r = 0;
-    }
-    r = (uint32_t)__shfl((int)r, 0, 64);
-    if (!r) return false;
-    Mask<NW> dd[1];
-    int mm[1];
-    double ll[1];
-    bool okk[1];
-    decode_chunks<M, TMAX, 1, false>(P, 64ull * (r - 1u), p.t, ex, lg, chien, ap, p.tab, dd, mm, ll, okk, 0ull);
-#pragma unroll
-    for (int s2 = 0; s2 < NW; ++s2) dn->diff[lane * NW + s2] = dd[0].w[s2];
-    dn->l[lane] = ll[0];
-    dn->m[lane] = (uint32_t)mm[0];
-    const uint64_t okm = ballot(okk[0]);
-    if (lane == 0) dn->okm = okm;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) lds_st(&ctl->redo_done, r);
-    if (lane == 0 && p.coop_stats) atomicAdd(p.coop_stats, 1u);
-    return true;
-}
-
 template <int M, int TMAX, bool TAB>
-__global__ void __launch_bounds__(kWaveSize * kCoopWaves)
+__global__ void __launch_bounds__(kWaveSize * coop_waves<M>())
 kaneko_coop_kernel(SearchParams p) {
     constexpr int NW = Geo<M>::NW;
     constexpr int NP = Smem<M, TMAX>::NP;
@@ -741,12 +780,34 @@ kaneko_coop_kernel(SearchParams p) {
     LongSlot<NW> *lring = reinterpret_cast<LongSlot<NW> *>(shared0);   // m >= 7
     LongDense<NW> *ldense = reinterpret_cast<LongDense<NW> *>(shared0 + sizeof(LongSlot<NW>) * kLongSlots);
     CoopCtl *ctl = reinterpret_cast<CoopCtl *>(shared0 + coop_ring_bytes<NW>());
-    uint8_t *wbase = reinterpret_cast<uint8_t *>(ctl + 1) + wid * Smem<M, TMAX>::WAVE_BYTES;
+    // n <= 63: a prep slice per wave; m >= 7: one shared slice, per-wave scratch, GfRep
+    uint8_t *area = reinterpret_cast<uint8_t *>(ctl + 1);
+    uint8_t *wbase = NW == 1 ? area + wid * Smem<M, TMAX>::WAVE_BYTES : area;
+    uint8_t *wscr = area + Smem<M, TMAX>::WAVE_BYTES + wid * kCoopScratch;  // m >= 7
+    uint8_t *grep = area + Smem<M, TMAX>::WAVE_BYTES + coop_waves<M>() * kCoopScratch;  // m >= 7
+    PrepTab<M, TMAX> *ptab =
+        reinterpret_cast<PrepTab<M, TMAX> *>(grep + (BCHK_LONG_GFREP ? gf_rep_bytes<M>() : 0));  // m >= 7
+    if constexpr (NW > 1 && BCHK_LONG_GFREP) {
+        __syncthreads();  // the packed tables are in LDS
+        gf_rep_fill<M>(grep, ex, lg);
+    }
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
     const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63) & ~63ull) : ~0ull;
     for (;;) {
+        // the lane index and t re-read opaquely per codeword: values derived from them are not
+        // hoisted out of this persistent loop (they stayed live through the whole body and
+        // spilled)
+        int lane_o = (int)(threadIdx.x & 63), t_o = p.t;
+        asm volatile("" : "+v"(lane_o), "+s"(t_o));
+        const int lane = lane_o, tt = t_o;
+#if BCHK_LONG_GFREP
+        const GfRep<M> gfr{grep, 4 * (lane & 15)};
+#else
+        const GfPlain<M> gfr{ex, lg};
+#endif
+        (void)tt;
         __syncthreads();
         if (threadIdx.x == 0) {
             ctl->item = next_heavy(p);
@@ -785,6 +846,8 @@ kaneko_coop_kernel(SearchParams p) {
             ctl->l0 = S.l0;
             ctl->skey = 0ull;
         }
+        if constexpr (NW > 1)  // the decoders' pattern tables (m >= 7)
+            if (wid == kAcceptor) prep_tab_store<M, TMAX>(ptab, P, lane);
         __syncthreads();
 #ifdef BCHK_DIAG
         unsigned long long t_prev = __builtin_amdgcn_s_memtime();
@@ -821,35 +884,47 @@ kaneko_coop_kernel(SearchParams p) {
         }
         if (NW > 1 && wid != kAcceptor) {
             // ------------------------------------------------ decoder, m >= 7 (packed)
-            for (bool fin = false; !fin;) {
-                uint32_t c = 0, nch = (uint32_t)kLongClaim;
-                if (lane == 0) {
-                    // the last BCHK_LONG_TAIL chunks below the published bound in smaller
-                    // claims: the codeword ends with its slowest claim
-                    if (BCHK_LONG_TAIL > 0) {
-                        const uint64_t bch = (lds_ld64(&ctl->bound) + 63ull) >> 6;
-                        if ((uint64_t)lds_ld(&ctl->next) + (uint64_t)BCHK_LONG_TAIL >= bch)
-                            nch = (uint32_t)BCHK_LONG_TAIL_CLAIM;
-                    }
-                    c = atomicAdd(&ctl->next, nch);
-                }
-                c = (uint32_t)__shfl((int)c, 0, 64);
-                nch = (uint32_t)__shfl((int)nch, 0, 64);
-                // wait for ring space, and while the claim lies past the published bound (it
-                // may rise again) or the cap: the codeword's end (done) releases the wave;
-                // dense requests are served meanwhile
+            // One call site of long_decode for both jobs: a dense re-decode the acceptor asks
+            // for (served first: it waits on it), else the wave's claim once it fits the ring
+            // and lies below the published loop bound (which may rise again) and the cap; the
+            // codeword's end (done) releases the wave. Nothing of the Prep is read here: the
+            // pattern tables are in LDS (PrepTab), so the decoders hold no prep registers.
+          if constexpr (NW > 1) {
+            bool have = false;
+            uint32_t c = 0, nch = (uint32_t)kLongClaim, spins = 0;
 #ifdef BCHK_DIAG
-                const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
+            unsigned long long tw0 = __builtin_amdgcn_s_memtime();
 #endif
-                for (uint32_t spins = 0;; ++spins) {
-                    if (lds_ld(&ctl->done)) { fin = true; break; }
-                    if constexpr (NW > 1)
-                        if (long_serve_redo<M, TMAX>(P, p, ctl, ldense, ex, lg, chien, ap, lane)) spins = 0;
-                    const uint64_t b0 = 64ull * c;
-                    if (c + (uint32_t)(kLongClaim - 1) < lds_ld(&ctl->consumed) + kLongSlots &&
-                        b0 < lds_ld64(&ctl->bound) && b0 < capc)
-                        break;
-                    if (spins > kSpinLimit) {
+            for (;;) {
+                if (!have) {
+                    if (lane == 0) {
+                        // the last BCHK_LONG_TAIL chunks below the published bound in smaller
+                        // claims: the codeword ends with its slowest claim
+                        nch = (uint32_t)kLongClaim;
+                        if (BCHK_LONG_TAIL > 0) {
+                            const uint64_t bch = (lds_ld64(&ctl->bound) + 63ull) >> 6;
+                            if ((uint64_t)lds_ld(&ctl->next) + (uint64_t)BCHK_LONG_TAIL >= bch)
+                                nch = (uint32_t)BCHK_LONG_TAIL_CLAIM;
+                        }
+                        c = atomicAdd(&ctl->next, nch);
+                    }
+                    c = (uint32_t)__shfl((int)c, 0, 64);
+                    nch = (uint32_t)__shfl((int)nch, 0, 64);
+                    have = true;
+                    spins = 0;
+                }
+                if (lds_ld(&ctl->done)) break;
+                uint32_t r = 0;  // a pending dense request (chunk + 1), taken by one wave
+                if (lane == 0) {
+                    r = lds_ld(&ctl->redo);
+                    if (r && atomicCAS(&ctl->redo, r, 0u) != r) r = 0;
+                }
+                r = (uint32_t)__shfl((int)r, 0, 64);
+                const uint64_t b0 = 64ull * c;
+                const bool ready = c + (uint32_t)(kLongClaim - 1) < lds_ld(&ctl->consumed) + kLongSlots &&
+                                   b0 < lds_ld64(&ctl->bound) && b0 < capc;
+                if (!r && !ready) {
+                    if (++spins > kSpinLimit) {
 #ifdef BCHK_COOP_DEBUG
                         if (lane == 0)
                             printf("dec wid %d cw %u claim %u consumed %u bound %llu done %u redo %u/%u next %u\n", wid, cw, c,
@@ -857,29 +932,39 @@ kaneko_coop_kernel(SearchParams p) {
                                    lds_ld(&ctl->done), lds_ld(&ctl->redo), lds_ld(&ctl->redo_done), lds_ld(&ctl->next));
 #endif
                         flag_fault(p, kFaultCoopRing);
-                        fin = true;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(2);
+                    continue;
                 }
 #ifdef BCHK_DIAG
                 const unsigned long long tw1 = __builtin_amdgcn_s_memtime();
                 dg[5] += tw1 - tw0;  // m >= 7 decoders: cycles waiting (ring space, bound, done)
 #endif
-                if (fin) break;
                 const double l0r = __longlong_as_double((long long)lds_ld64(
                     reinterpret_cast<const uint64_t *>(&ctl->l0)));
                 const uint64_t skey = lds_ld64(&ctl->skey);  // a codeword found before chunk c
-                int rounds = 0;
-                if constexpr (NW > 1)
-                    rounds = long_decode_claim<M, TMAX>(P, c, capc, ~0ull, l0r, skey, p.t, ex, lg, chien, ap, as, lring,
-                                                        ctl, lane, nch, p.long_rec);
+                const bool dense = r != 0u;
+                const int rounds = long_decode<M, TMAX>(ptab, ordl, dense ? r - 1u : c, capc, l0r, skey, tt, ex, gfr,
+                                                        ap, wscr, lring, ldense, ctl, lane, dense ? 1u : nch,
+                                                        p.long_rec, dense);
+                if (dense) {
+                    if (lane == 0) {
+                        lds_st(&ctl->redo_done, r);
+                        if (p.coop_stats) atomicAdd(p.coop_stats, 1u);
+                    }
+                } else {
+                    have = false;
+                }
+                spins = 0;
 #ifdef BCHK_DIAG
                 dg[3] += (unsigned long long)rounds;  // m >= 7: decode rounds of 64 packed patterns
-                dg[4] += __builtin_amdgcn_s_memtime() - tw1;  // m >= 7 decoders: cycles in claims
+                tw0 = __builtin_amdgcn_s_memtime();
+                dg[4] += tw0 - tw1;  // m >= 7 decoders: cycles in claims
 #endif
                 (void)rounds;
             }
+          }
         } else if (wid != kAcceptor) {
             // ------------------------------------------------------------ decoder
             constexpr int G = chunk_group<TAB>();
@@ -1265,7 +1350,7 @@ static hipError_t launch_search_impl(const SearchParams &p, int grid, size_t lds
 }
 template <int M, int TMAX, bool TAB>
 static hipError_t launch_coop_impl(const SearchParams &p, int grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((kaneko_coop_kernel<M, TMAX, TAB>), dim3(grid), dim3(kWaveSize * kCoopWaves),
+    hipLaunchKernelGGL((kaneko_coop_kernel<M, TMAX, TAB>), dim3(grid), dim3(kWaveSize * coop_waves<M>()),
                        lds, s, p);
     return hipGetLastError();
 }
@@ -1316,8 +1401,7 @@ bool select_first_long(int m, int t, FastFn *out) {
 template <int M, int TMAX>
 static KernelSet make_set() {
     constexpr int NW = Geo<M>::NW;
-    const size_t coop = coop_ring_bytes<NW>() + sizeof(CoopCtl) +
-                        (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES;
+    const size_t coop = coop_ring_bytes<NW>() + sizeof(CoopCtl) + coop_wave_area<M, TMAX>();
     KernelSet k{};
     k.search = &launch_search_impl<M, TMAX, false, false>;
     k.coop = &launch_coop_impl<M, TMAX, false>;
@@ -1339,6 +1423,7 @@ static KernelSet make_set() {
         k.tail_wave_bytes = (size_t)(Smem<M, TMAX>::WAVE_BYTES + an_bytes<M, TMAX>());
         k.tail_block_bytes = (size_t)help_bytes<M, TMAX>();
     }
+    k.coop_threads = kWaveSize * coop_waves<M>();
     k.coop_bytes = coop;
     k.alg = &launch_alg_impl<M, TMAX>;
     k.tmax = TMAX;

@@ -30,6 +30,7 @@ struct KernelSet {
     const void *(*tail_tab_ptr)();
     size_t tail_wave_bytes;
     size_t tail_block_bytes;  // the block's helper-job control (HelpCtl) after the waves
+    int coop_threads;         // the cooperative kernel's workgroup size
 };
 
 typedef hipError_t (*FastFn)(const SearchParams &, size_t, hipStream_t);
