@@ -139,7 +139,9 @@ struct SearchParams {
     // fast ring kernel (bchk_fast.hip): waves per workgroup (0: all 16 -- 1 loader + 15
     // compute; fewer leave room for a concurrent kernel), and experiment modes (0: normal;
     // 1: the loader publishes slots without loading them, 2: compute waves only read their
-    // slot -- timing builds of the two halves, wrong results)
+    // slot -- timing builds of the two halves, wrong results; 3: the slot held through the
+    // i = 0 tests, 6: flipped positions' values all re-read from HBM -- correct, slower or
+    // more bytes, measured)
     uint32_t fast_waves;
     uint32_t fast_mode;
     // cooperative kernel, m >= 7: candidate records a ring slot keeps (0..2; a chunk with more

@@ -185,11 +185,14 @@ __device__ __forceinline__ void fast_sort64(uint32_t (&key)[64], uint32_t &kmax_
 
 // The decision from the sorted prefix k[0..15] (ranks 0..15 of the 64 keys), the largest
 // real key and the sorter's flags: returned at i = 0 / i = 1, or unresolved.
-template <int M, int TMAX>
+// Row values are read through rd0 for the i = 0 tests and through rd1 for i = 1; `between`
+// runs after the i = 0 tests (the ring kernel gives its LDS slot back there).
+template <int M, int TMAX, class Rd0, class Rd1, class Between>
 __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t *lg, const uint32_t *col,
                                                const uint64_t *chien, const uint32_t *k, uint32_t kmax_real,
-                                               bool bad, uint64_t yH, const double *yrow, bool live, int t,
-                                               double s2) {
+                                               bool bad, uint64_t yH, Rd0 rd0, Rd1 rd1, Between between,
+                                               bool live, int t, double s2, const uint32_t *lo = nullptr,
+                                               bool have_lo = false) {
     constexpr int N = Geo<M>::N;
     constexpr int W = (TMAX + 3) / 4;
     // calcRightSide takes the first border = 2t+1-m agreeing sorted positions; with m0 == m
@@ -236,7 +239,7 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
     }
     // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`
     // (at most t + 1 positions: the error pattern, plus the flipped bit at i = 1).
-    auto accept = [&](uint64_t diff, double &l, bool &ret) {
+    auto accept = [&](auto rd, uint64_t diff, double &l, bool &ret) {
         constexpr int LMAX = TMAX + 1;
         const int m = __popcll(diff);
         const int border = (2 * t + 1) - m;  // m0 == m on both fast-path exits
@@ -245,7 +248,22 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
 #pragma unroll
         for (int j = 0; j < LMAX; ++j) {  // independent loads, issued together; only the
             g[j] = 0.0;                    // flipped positions' (no line fetched for others)
-            if (v) g[j] = yrow[(int)__builtin_ctzll(v)];
+            const int pj = (int)__builtin_ctzll(v);
+            bool found = false;
+            if (have_lo) {
+                // |y| of a prefix rank rebuilt exactly: its key's exponent and 21 mantissa bits
+                // (the hi word's 20 below the top) and the row's lo word, gathered before the
+                // slot was given back (a non-bad key: 2^-27 <= |y| < 32)
+                uint64_t bits = 0;
+#pragma unroll
+                for (int r = 0; r < NPF; ++r) {
+                    const bool hit = (pre[r] & 63u) == (uint32_t)pj;
+                    found = found || hit;
+                    bits = hit ? ((uint64_t)((pre[r] >> 7) + (996u << 20)) << 32) | lo[r] : bits;
+                }
+                if (v) g[j] = __longlong_as_double((long long)bits);
+            }
+            if (v && !found) g[j] = rd(pj);
             v &= v - 1;
         }
         l = 0.0;
@@ -282,7 +300,7 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
     if (!bad && ok0) {
         double l;
         bool ret;
-        accept(E.w[0], l, ret);
+        accept(rd0, E.w[0], l, ret);
         if (ret) { R.state = 1; R.best = E.w[0]; R.l0 = l; }
     }
     // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371). When the
@@ -295,9 +313,10 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
     if (live && !bad && !ok0 && zero0) {
         double l;
         bool ret;
-        accept(0ull, l, ret);
+        accept(rd0, 0ull, l, ret);
         if (ret) { R.state = 2; R.best = 0ull; R.l0 = l; }
     }
+    between();
     const bool need1 = live && !bad && !ok0 && !zero0;
     if (ballot(need1)) {
         uint32_t S1[W];
@@ -308,7 +327,7 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
             const uint64_t diff = (1ull << o0) ^ E.w[0];
             double l;
             bool ret;
-            accept(diff, l, ret);
+            accept(rd1, diff, l, ret);
             if (ret) { R.state = 2; R.best = diff; R.l0 = l; }
         }
     }
@@ -466,7 +485,9 @@ kaneko_fast_kernel(SearchParams p) {
     uint32_t kmax_real;
     bool bad;
     fast_sort64<M, TMAX, SEL>(key, kmax_real, bad);
-    const FastRes R = fast_decide<M, TMAX>(ex, lg, col, chien, key, kmax_real, bad, yH, yrow, live, p.t, p.s2);
+    auto rdg = [&](int pos) { return yrow[pos]; };
+    const FastRes R = fast_decide<M, TMAX>(ex, lg, col, chien, key, kmax_real, bad, yH, rdg, rdg, [] {}, live,
+                                           p.t, p.s2);
 
     // ---- outputs: resolved rows through LDS, one coalesced 64-row block per wave. The
     // unresolved rows of the block are read back and written unchanged (the exact kernel,
@@ -716,31 +737,54 @@ kaneko_fast_ring_kernel(SearchParams p) {
                 }
             }
         };
+        typedef __attribute__((address_space(3))) const double *LdsF64;
+        LdsF64 lrow = (LdsF64)(ring + s * SLOT);  // a C cast: generic -> LDS address space
+        lrow += lane * N;
+        const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
         if (full) {  // the slot (LDS)
-            typedef __attribute__((address_space(3))) const double *LdsF64;
-            LdsF64 row = (LdsF64)(ring + s * SLOT);  // a C cast: generic -> LDS address space
-            row += lane * N;
-            build([&](int pos) { return row[pos]; });
+            build([&](int pos) { return lrow[pos]; });
         } else {     // the partial last chunk, from HBM
-            const double *row = p.y + (size_t)(live ? cw : cw0) * N;
-            build([&](int pos) { return row[pos]; });
+            build([&](int pos) { return yrow[pos]; });
         }
-        // every read of the slot has returned (its values are in the keys): give it back
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        wave_sync();
-        if (lane == 0) lds_st32(&ctl->tag[s], 0u);
+        // the slot goes back once every read of it has returned: now (the tests rebuild the
+        // prefix ranks' values from their keys and lo words; other flipped positions' values
+        // are read again from HBM), or in experiment mode 3 after the i = 0 tests, which
+        // then read them from the slot (the slot is held through the decode: slower, measured)
+        // the lo words of the prefix ranks' values (the accept tests rebuild those exactly:
+        // re-reading a flipped position from HBM fetches a 128-B line the stream has long
+        // evicted from L2 -- 0.32 GB per 2^20 rows at 5 dB, measured; experiment mode 6 does)
+        constexpr int NPF = KMAX + 1;
+        uint32_t lo[NPF] = {};
+        const bool use_lo = full && p.fast_mode != 6u;
+        if (use_lo) {
+            typedef __attribute__((address_space(3))) const uint32_t *LdsU32;
+            LdsU32 lw = (LdsU32)(ring + s * SLOT);
+            lw += lane * 2 * N;
+#pragma unroll
+            for (int r = 0; r < NPF; ++r) lo[r] = lw[2 * (kept[r] & 63u)];
+        }
+        auto release = [&] {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            wave_sync();
+            if (lane == 0) lds_st32(&ctl->tag[s], 0u);
+        };
+        const bool hold = full && p.fast_mode == 3u;
+        if (!hold) release();
         const uint64_t yH = hard_decision<N>(yHl, yHh);
         if (p.fast_mode == 2u) {  // experiment: the rows' path alone (wrong results)
+            if (hold) release();
             if (p.l0 && live) p.l0[cw] = (double)(kept[3] ^ kmax_real ^ (uint32_t)yH);
             continue;
         }
-        const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
         // t and s2 re-read opaquely per chunk: nothing derived from them is hoisted out of
         // the persistent loop (it would stay live through the selection and spill)
         int t = p.t;
         double s2 = p.s2;
         asm volatile("" : "+s"(t), "+s"(s2));
-        const FastRes R = fast_decide<M, TMAX>(ex, lg, col, chien, kept, kmax_real, false, yH, yrow, live, t, s2);
+        const FastRes R = fast_decide<M, TMAX>(
+            ex, lg, col, chien, kept, kmax_real, false, yH, [&](int pos) { return hold ? lrow[pos] : yrow[pos]; },
+            [&](int pos) { return yrow[pos]; }, [&] { if (hold) release(); }, live, t, s2,
+            lo, use_lo);
 
         // ---- outputs
         const bool resolved = live && R.state != 0;

@@ -774,7 +774,8 @@ kaneko_coop_kernel(SearchParams p) {
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
     const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
     const uint64_t *chien = reinterpret_cast<const uint64_t *>(smem + p.td.off_chien);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    [[maybe_unused]] const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
     uint8_t *shared0 = smem + ((p.td.bytes + 15) & ~15u);
     CoopSlot<NW> *ring = reinterpret_cast<CoopSlot<NW> *>(shared0);    // n <= 63
     LongSlot<NW> *lring = reinterpret_cast<LongSlot<NW> *>(shared0);   // m >= 7

@@ -15,6 +15,23 @@ for cfg in "$@"; do
   timeout -k 10 200 env $ENVS python scripts/fast_probe.py $ARGS --tag "$ENVS" >> $OUT/${TAG}_probe.jsonl 2>> $OUT/${TAG}_probe.err
   rc=$?; echo "[$cfg] rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
+if [ -n "${REQ:-}" ]; then
+  # memory-side requests by size (reads, then writes) of the decode call, per configuration
+  cd /tmp && export TMPDIR=/tmp
+  j=0
+  for cfg in "$@"; do
+    j=$((j+1)); ENVS=${cfg%%|*}; ARGS=${cfg#*|}
+    i=0
+    for CNT in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
+               "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_HIT_sum TCC_MISS_sum"; do
+      i=$((i+1))
+      timeout -s KILL 120 env $ENVS rocprofv3 --pmc $CNT --kernel-trace --output-format csv -d $OUT/${TAG}_req${j}_$i -o run \
+          -- python3 $ROOT/scripts/fast_probe.py --steps 2 $ARGS > $OUT/${TAG}_req${j}_$i.log 2>&1
+      rc=$?; echo "req cfg $j pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    done
+  done
+  cd $ROOT
+fi
 if [ -n "${PMC:-}" ]; then
   cd /tmp && export TMPDIR=/tmp
   i=0

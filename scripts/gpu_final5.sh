@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 artefacts: all GPU tests, the default bench line (CPU baseline), rocprofv3 kernel
-# stats and PMC HBM traffic of the headline; optionally (CONFIG5=1) config 5's lines with
+# stats and memory-side traffic (PMC requests by size) of the headline; optionally (CONFIG5=1) config 5's lines with
 # their PMC traffic and CPU baseline. Every GPU step under its own limit; stops at a failure.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -13,19 +13,19 @@ if [ -z "${SKIP_TESTS:-}" ]; then
   rc=$?; echo "tests rc=$rc"; tail -n 2 $OUT/tests_$TAG.log
   [ $rc -eq 0 ] || exit $rc
 fi
-pmc() {  # name, bench args: FETCH_SIZE and WRITE_SIZE passes, each its own run
+pmc() {  # name, bench args: memory-side requests by size (reads, then writes), each pass its own run
   local nm=$1; shift
   local i=0
-  for CNT in FETCH_SIZE WRITE_SIZE; do
+  for CNT in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
+             "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"; do
     i=$((i+1))
     timeout -s KILL 150 rocprofv3 --pmc $CNT --kernel-trace --output-format csv -d $OUT/traffic_${nm}_p$i -o run \
         -- python3 $ROOT/bench.py --steps 2 --warmup 1 --cpu-seconds 0 --points '' "$@" > $OUT/traffic_${nm}_p$i.log 2>&1
-    rc=$?; echo "pmc $nm pass $i ($CNT) rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    rc=$?; echo "pmc $nm pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
-  python3 $ROOT/scripts/pmc_summary.py $OUT/traffic_$nm > $OUT/traffic_${nm}_summary.json || exit 1
 }
 ( cd /tmp && export TMPDIR=/tmp && pmc $TAG --snr 5 ) || exit 1
-python3 $ROOT/scripts/traffic_json.py $OUT/traffic_${TAG}_summary.json 1048576 5.0 15 > $OUT/traffic_${TAG}.json && echo traffic json ok
+python3 $ROOT/scripts/traffic_req_json.py $OUT/traffic_${TAG}_p1/run_counter_collection.csv $OUT/traffic_${TAG}_p2/run_counter_collection.csv 1048576 5.0 15 > $OUT/traffic_${TAG}.json && echo traffic json ok
 timeout -k 10 300 python bench.py --traffic $OUT/traffic_${TAG}.json > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
@@ -39,7 +39,7 @@ for PT in "5 15" "6 -1" "7 15"; do
   set -- $PT
   nm=${TAG}_255_${1}dB
   ( cd /tmp && export TMPDIR=/tmp && pmc $nm --m 8 --t 15 --snr $1 --J $2 ) || exit 1
-  python3 $ROOT/scripts/traffic_json.py $OUT/traffic_${nm}_summary.json 1048576 $1.0 $2 > $OUT/traffic_${nm}.json
+  python3 $ROOT/scripts/traffic_req_json.py $OUT/traffic_${nm}_p1/run_counter_collection.csv $OUT/traffic_${nm}_p2/run_counter_collection.csv 1048576 $1.0 $2 > $OUT/traffic_${nm}.json
   timeout -k 10 400 python bench.py --m 8 --t 15 --snr $1 --J $2 --points '' --steps 5 --warmup 1 --cpu-seconds 12 \
       --traffic $OUT/traffic_${nm}.json >> $OUT/${TAG}_255.jsonl 2>> $OUT/${TAG}_255.err
   rc=$?; echo "[255 $PT] rc=$rc"; [ $rc -eq 0 ] || exit $rc

@@ -27,7 +27,8 @@ def per_launch(path):
 
 rd, wr = per_launch(sys.argv[1]), per_launch(sys.argv[2])
 res = {"batch": int(sys.argv[3]), "snr_db": float(sys.argv[4]), "J": int(sys.argv[5]),
-       "source": f"{sys.argv[1]} + {sys.argv[2]} (TCC_EA0_RDREQ/WRREQ by request size)",
+       "source": f"{sys.argv[1].split('gpurun_out/')[-1]} + {sys.argv[2].split('gpurun_out/')[-1]} "
+                 "(TCC_EA0_RDREQ/WRREQ by request size)",
        "date": datetime.date.today().isoformat(), "kernels": {}, "read_bytes": {}, "write_bytes": {}}
 for k in sorted(set(rd) & set(wr)):
     r, w = rd[k], wr[k]
