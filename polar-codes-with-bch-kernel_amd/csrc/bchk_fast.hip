@@ -18,6 +18,7 @@
 // queue that the wave-per-codeword kernel (bchk_kernels.hip) processes from scratch, so
 // every result is the reference's.
 #include <algorithm>
+#include <cfloat>
 #include <cstdlib>
 
 #include "bchk_core.h"
@@ -914,6 +915,364 @@ static hipError_t launch_fast_impl(const SearchParams &p, size_t lds, hipStream_
         }
     }
     return launch_fast_sel<M, TMAX, false>(p, lds, s);
+}
+
+// ---------------------------------------------------------------------------------------
+// Long codes (m >= 7, TMAX <= 15): the lane-per-codeword pre-pass of kaneko_first_kernel.
+// The wave-per-codeword first kernel spends ~1 700 wave instructions on each codeword (a
+// 64-lane selection network, cross-lane syndromes and key equations) although at the SNRs
+// of use nearly every codeword returns at test pattern 0 or 1. This kernel gives each lane
+// one codeword of a 64-row chunk and decides exactly those two exits, as the n <= 63 fast
+// kernel does (fast_decide: the same certified tests), and marks the rows it finished in
+// pre_mask; the first kernel then takes only the others, from scratch.
+//   - rows stream through a per-wave LDS buffer 16 positions at a time (8-B loads, four
+//     rows of 128 contiguous bytes per wave instruction; the next segment's loads are in
+//     flight while this one is keyed), each lane reading its own row back;
+//   - 32-bit keys: a 24-bit monotone prefix of |y| (5 exponent bits over [2^-27, 2^5), 19
+//     mantissa bits) above the 8-bit position; the 32 smallest are kept sorted (Green's
+//     16-key network per segment, then a bitonic merge into the kept 32), which covers the
+//     ranks KMAX + 2 <= 32 the decision reads;
+//   - hard-decision syndromes from the LDS column table; the decodes per lane
+//     (alg_decode_lanes: binary BM, split test, wave-spread Chien scan of each success).
+constexpr int kLaneWaves = 8;                   // waves per workgroup (2 workgroups per CU)
+constexpr int kLaneSeg = 16;                    // positions per staged segment
+constexpr int kLaneRowD = kLaneSeg + 1;         // doubles per staged row (pad: b64 reads spread)
+constexpr int kLaneWaveBytes = 64 * kLaneRowD * 8;
+constexpr int kLaneKeep = 32;
+
+// 24-bit prefix (5 exponent bits, 19 mantissa bits; 0: |y| < 2^-27 or zero, all ones:
+// |y| >= 32, inf, NaN) above the 8-bit position
+__device__ __forceinline__ uint32_t sort_key8(uint32_t hi, int pos) {
+    const uint32_t ahi = hi & 0x7FFFFFFFu;
+    const uint32_t d = __builtin_elementwise_sub_sat(ahi, (uint32_t)(1023 - 27) << 20) >> 1;
+    const uint32_t pre = d < 0xFFFFFFu ? d : 0xFFFFFFu;
+    return (pre << 8) | (uint32_t)pos;
+}
+
+// kept[0..32) and nk[0..16) sorted -> kept = the 32 smallest of both, sorted: kept with the
+// reversed nk (padded with +inf) taken elementwise by min is bitonic, then a bitonic merge
+__device__ __forceinline__ void merge_low32_16(uint32_t (&kept)[32], const uint32_t (&nk)[16]) {
+#pragma unroll
+    for (int i = 16; i < 32; ++i) {
+        const uint32_t a = kept[i], b = nk[31 - i];
+        kept[i] = a < b ? a : b;
+    }
+    uint32_t *key = kept;
+#pragma unroll
+    for (int j = 16; j > 0; j >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+            if (!(i & j)) BCHK_CAS(i, i + j)
+    }
+}
+
+template <int NW>
+struct LaneRes {
+    int state;  // 0 unresolved, 1 returned at i = 0, 2 returned at i = 1
+    Mask<NW> best;
+    double l0;
+};
+
+// bit pos of a mask: the words masked arithmetically (a select chain over the words is
+// turned into a dynamically indexed stack copy -- scratch)
+template <int NW>
+__device__ __forceinline__ bool mask_bit(const Mask<NW> &m, int pos) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const uint32_t in = (uint32_t)((pos >> 6) == s);
+        b |= (uint32_t)(m.w[s] >> (pos & 63)) & in;
+    }
+    return b & 1u;
+}
+
+// fast_decide for n <= 255 (NW words): the same exits, tests and bounds from k[0..KMAX+1]
+template <int M, int TMAX>
+__device__ __forceinline__ LaneRes<Geo<M>::NW> lane_decide(const uint8_t *ex, const uint16_t *lg, const uint32_t *col,
+                                                           const uint32_t (&k)[kLaneKeep], uint32_t kmax_real,
+                                                           const Mask<Geo<M>::NW> &yH, const double *yrow, bool live,
+                                                           int t, double s2) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    constexpr int W = (TMAX + 3) / 4;
+    constexpr int KMAX = 2 * TMAX;
+    static_assert(KMAX + 2 <= kLaneKeep, "the kept keys cover the decision's ranks");
+    constexpr int NPF = KMAX + 1;
+    bool bad = (k[0] >> 8) == 0u || (kmax_real >> 8) == 0xFFFFFFu;
+#pragma unroll
+    for (int r = 0; r < KMAX + 1; ++r) bad |= ((k[r] ^ k[r + 1]) >> 8) == 0u;
+    uint32_t pre[NPF];
+#pragma unroll
+    for (int r = 0; r < NPF; ++r) pre[r] = k[r];
+    const int o0 = (int)(k[0] & 255u);
+    const double c2 = 2.0 / s2;
+    // syndrome of the hard decision (Decoder::findSyndromPoly :184-207): uniform positions,
+    // broadcast column reads
+    uint32_t S0[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) S0[w] = 0;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const uint32_t lo32 = (uint32_t)yH.w[s], hi32 = (uint32_t)(yH.w[s] >> 32);
+#pragma unroll 8
+        for (int b = 0; b < 64; ++b) {
+            const int pos = 64 * s + b;
+            if (pos < N) {
+                const uint32_t on = (uint32_t)((int32_t)((b < 32 ? lo32 << (31 - b) : hi32 << (63 - b))) >> 31);
+#pragma unroll
+                for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w] & on;
+            }
+        }
+    }
+    // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`, as
+    // fast_decide's accept
+    auto accept = [&](const Mask<NW> &diff, double &l, bool &ret) {
+        constexpr int LMAX = TMAX + 1;
+        const int m = mask_popc<NW>(diff);
+        const int border = (2 * t + 1) - m;
+        double g[LMAX];
+        Mask<NW> v = diff;
+#pragma unroll
+        for (int j = 0; j < LMAX; ++j) {  // the j-th flipped position, ascending
+            int pj = -1;
+#pragma unroll
+            for (int s = NW - 1; s >= 0; --s)
+                if (v.w[s]) pj = 64 * s + (int)__builtin_ctzll(v.w[s]);
+#pragma unroll
+            for (int s = 0; s < NW; ++s)
+                if ((pj >> 6) == s && pj >= 0) v.w[s] &= v.w[s] - 1;
+            g[j] = 0.0;
+            if (pj >= 0) g[j] = yrow[pj];
+        }
+        l = 0.0;
+#pragma unroll
+        for (int j = 0; j < LMAX; ++j)
+            if (j < m) l += fabs((2.0 * g[j]) / s2);
+        double rs_lo = 0.0;
+        int taken = 0;
+#pragma unroll
+        for (int r = 0; r < NPF; ++r) {
+            const bool ag = !mask_bit<NW>(diff, (int)(pre[r] & 255u));
+            if (ag && taken < border) {
+                const uint32_t pr = pre[r] >> 8;  // eb (5 bits) | 19 mantissa bits
+                const uint64_t bits = (uint64_t)((pr << 1) + (996u << 20)) << 32;
+                rs_lo += __longlong_as_double((long long)bits) * c2;
+                ++taken;
+            }
+        }
+        ret = (taken >= border) && (m <= LMAX) && (l < rs_lo * (1.0 - 0x1p-40));
+    };
+
+    LaneRes<NW> R;
+    R.state = 0;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) R.best.w[s] = 0;
+    R.l0 = DBL_MAX;
+    bool zero0 = true;
+#pragma unroll
+    for (int w = 0; w < W; ++w) zero0 = zero0 && S0[w] == 0u;
+    Mask<NW> E;
+    const bool ok0 = alg_decode_lanes<M, TMAX>(ex, lg, S0, t, E, live && !bad && !zero0);
+    if (live && !bad && ok0) {
+        double l;
+        bool ret;
+        accept(E, l, ret);
+        if (ret) { R.state = 1; R.best = E; R.l0 = l; }
+    }
+    // i = 1 where i = 0 failed (:371): a codeword hard decision (zero syndrome) returns to
+    // itself (D = 0, l = 0); otherwise pattern 1 flips rank 0 and is decoded
+    if (live && !bad && !ok0 && zero0) {
+        Mask<NW> z;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) z.w[s] = 0;
+        double l;
+        bool ret;
+        accept(z, l, ret);
+        if (ret) { R.state = 2; R.l0 = l; }
+    }
+    const bool need1 = live && !bad && !ok0 && !zero0;
+    if (ballot(need1)) {
+        uint32_t S1[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) S1[w] = S0[w] ^ col[o0 * W + w];
+        const bool ok1 = alg_decode_lanes<M, TMAX>(ex, lg, S1, t, E, need1);
+        if (need1 && ok1) {
+            Mask<NW> diff = E;
+#pragma unroll
+            for (int s = 0; s < NW; ++s) diff.w[s] ^= (o0 >> 6) == s ? 1ull << (o0 & 63) : 0ull;
+            double l;
+            bool ret;
+            accept(diff, l, ret);
+            if (ret) { R.state = 2; R.best = diff; R.l0 = l; }
+        }
+    }
+    return R;
+}
+
+template <int M, int TMAX>
+__global__ void __launch_bounds__(kWaveSize * kLaneWaves) kaneko_lane_kernel(SearchParams p) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    constexpr int NSEG = (N + kLaneSeg - 1) / kLaneSeg;
+    static_assert(kLaneSeg == 16, "segment = four rows of 16 positions per wave instruction");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    load_tables(smem, p.tables, p.td.bytes);
+    __syncthreads();
+    const uint8_t *ex = smem + p.td.off_exp;
+    const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
+    const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint8_t *wb = smem + ((p.td.bytes + 15) & ~15u) + wid * kLaneWaveBytes;
+    double *seg = reinterpret_cast<double *>(wb);
+    const uint32_t gk = blockIdx.x * kLaneWaves + (uint32_t)wid;  // this wave's chunk
+    const uint32_t nch = (p.count + 63u) / 64u;
+    if (gk >= nch) return;
+    const uint32_t cw0 = 64u * gk, cw = cw0 + (uint32_t)lane;
+    const bool live = cw < p.count;
+    const uint32_t rows = p.count - cw0 < 64u ? p.count - cw0 : 64u;
+    // segment loads: instruction i, lane l -> row 4 i + l / 16, position 16 g + l % 16
+    const int lr = lane >> 4, lj = lane & 15;
+    double pf[16];
+    auto load_seg = [&](int g) {
+        const int pos = kLaneSeg * g + lj;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t r = 4u * i + (uint32_t)lr;
+            pf[i] = (pos < N && r < rows) ? p.y[(size_t)(cw0 + r) * N + pos] : 0.0;
+        }
+    };
+    load_seg(0);
+    uint32_t kept[kLaneKeep];
+#pragma unroll
+    for (int i = 0; i < kLaneKeep; ++i) kept[i] = 0xFFFFFFFFu;
+    uint32_t kmax_real = 0;
+    Mask<NW> yH;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) yH.w[s] = 0;
+#pragma nounroll
+    for (int g = 0; g < NSEG; ++g) {
+        wave_sync();  // the previous segment's reads are done
+#pragma unroll
+        for (int i = 0; i < 16; ++i) seg[(4 * i + lr) * kLaneRowD + lj] = pf[i];
+        wave_sync();
+        if (g + 1 < NSEG) load_seg(g + 1);
+        uint32_t nk[16];
+        uint32_t sb = 0;  // sign bits of the segment (position 16 g + i -> bit i)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int pos = kLaneSeg * g + i;
+            const uint64_t bb = (uint64_t)__double_as_longlong(seg[lane * kLaneRowD + i]);
+            const uint32_t hi = (uint32_t)(bb >> 32);
+            nk[i] = pos < N ? sort_key8(hi, pos) : 0xFFFFFFFFu;
+            sb |= (pos < N ? (~hi >> 31) : 0u) << i;
+        }
+        sort16<0>(nk);
+        const int cnt = N - kLaneSeg * g > 16 ? 16 : N - kLaneSeg * g;
+        uint32_t top = nk[15];
+#pragma unroll
+        for (int i = 0; i < 15; ++i) top = cnt == i + 1 ? nk[i] : top;
+        kmax_real = top > kmax_real ? top : kmax_real;
+        merge_low32_16(kept, nk);
+        // y > 0 is the clear sign bit (the hard decision, :336-342); y = +0 has prefix 0 and
+        // is sent to the slow path by lane_decide
+#pragma unroll
+        for (int s = 0; s < NW; ++s)
+            yH.w[s] |= (g >> 2) == s ? (uint64_t)sb << (16 * (g & 3)) : 0ull;
+    }
+    int t = p.t;
+    double s2 = p.s2;
+    asm volatile("" : "+s"(t), "+s"(s2));
+    const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
+    const LaneRes<NW> R = lane_decide<M, TMAX>(ex, lg, col, kept, kmax_real, yH, yrow, live, t, s2);
+
+    // ---- outputs: decoded rows of the finished codewords (others untouched: the first
+    // kernel writes them), their l0, the fused counters and the chunk's pre_mask word
+    const bool resolved = live && R.state != 0;
+    Mask<NW> x;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) x.w[s] = yH.w[s] ^ R.best.w[s];
+    uint32_t e = 0;
+    uint8_t *dst = p.res + (size_t)cw0 * N;
+    const uint8_t *txb = p.tx ? p.tx + (size_t)cw0 * N : nullptr;
+    wave_sync();  // the segment buffer becomes the masks' area
+    uint64_t *xm = reinterpret_cast<uint64_t *>(wb);            // [64][NW]
+    uint32_t *rowerr = reinterpret_cast<uint32_t *>(wb + 64 * NW * 8);
+    if (rows == 64u && ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(txb)) & 15u) == 0) {
+        const uint64_t rm = ballot(resolved);
+#pragma unroll
+        for (int s = 0; s < NW; ++s) xm[lane * NW + s] = x.w[s];
+        rowerr[lane] = 0u;
+        wave_sync();
+        bool anyerr = false;
+        for (int q = lane; q < 4 * N; q += 64) {
+            const int b0 = 16 * q, r1 = b0 / N, o = b0 - N * r1;
+            const bool span = o > N - 16;
+            const int r2 = span ? r1 + 1 : r1;
+            const int wi = o >> 6, sh = o & 63;
+            const uint64_t a0 = xm[r1 * NW + wi];
+            const uint64_t a1 = (wi + 1 < NW && sh) ? xm[r1 * NW + wi + 1] : 0ull;
+            uint64_t w = (a0 >> sh) | (sh ? a1 << (64 - sh) : 0ull);
+            if (span) w = (w & ((1ull << (N - o)) - 1ull)) | (xm[r2 * NW] << (N - o));
+            uint32_t nw[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) nw[d] = nib_bytes((uint32_t)(w >> (4 * d)) & 15u);
+            const uint32_t in2 = span ? (0xFFFFu << (N - o)) & 0xFFFFu : 0u;
+            const uint32_t keep = (((rm >> r1) & 1ull) ? 0u : (~in2 & 0xFFFFu)) |
+                                  (((rm >> r2) & 1ull) ? 0u : in2);
+            if (!keep) {
+                reinterpret_cast<uint4 *>(dst)[q] = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+            } else if (keep != 0xFFFFu) {
+                for (uint32_t wm = ~keep & 0xFFFFu; wm; wm &= wm - 1) {
+                    const int i = __builtin_ctz(wm);
+                    dst[16 * q + i] = (uint8_t)(nw[i >> 2] >> (8 * (i & 3)));
+                }
+            }
+            if (txb) {
+                const uint4 a = reinterpret_cast<const uint4 *>(txb)[q];
+                const uint32_t xx[4] = {a.x ^ nw[0], a.y ^ nw[1], a.z ^ nw[2], a.w ^ nw[3]};
+                if (xx[0] | xx[1] | xx[2] | xx[3]) {
+                    anyerr = true;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if ((xx[i >> 2] >> (8 * (i & 3))) & 0xFFu) atomicAdd(&rowerr[i < N - o ? r1 : r2], 1u);
+                }
+            }
+        }
+        if (txb && ballot(anyerr)) {
+            wave_sync();
+            e = resolved ? rowerr[lane] : 0u;
+        }
+    } else if (resolved) {  // partial chunk (or unaligned buffers): the row byte by byte
+        for (int pos = 0; pos < N; ++pos) {
+            const uint8_t bit = mask_bit<NW>(x, pos) ? 1u : 0u;
+            dst[lane * N + pos] = bit;
+            if (txb) e += txb[lane * N + pos] != bit ? 1u : 0u;
+        }
+    }
+    if (p.cnt) fast_counters(p, cw0, N, resolved, R.state, e);
+    if (resolved && p.l0) p.l0[cw] = R.l0;
+    const uint64_t done = ballot(resolved);
+    if (lane == 0) p.pre_mask[gk] = done;
+}
+
+template <int M, int TMAX>
+static hipError_t launch_lane_impl(const SearchParams &p, size_t, hipStream_t s) {
+    const uint32_t chunks = (p.count + 63u) / 64u;
+    const int blocks = (int)((chunks + kLaneWaves - 1) / kLaneWaves);
+    const size_t lds = ((p.td.bytes + 15) & ~size_t(15)) + (size_t)kLaneWaves * kLaneWaveBytes;
+    static bool attr = false;
+    if (!attr && lds > 65536) {
+        (void)hipFuncSetAttribute((const void *)&kaneko_lane_kernel<M, TMAX>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    if (blocks > 0) hipLaunchKernelGGL((kaneko_lane_kernel<M, TMAX>), dim3(blocks), dim3(kWaveSize * kLaneWaves), lds, s, p);
+    return hipGetLastError();
+}
+
+// the same (m, TMAX) buckets as select_first_long (the column table's stride)
+bool select_lane(int m, int t, FastFn *out) {
+    if (m == 7 && t <= 8) { *out = &launch_lane_impl<7, 8>; return true; }
+    if (m == 8 && t <= 15) { *out = &launch_lane_impl<8, 15>; return true; }
+    return false;
 }
 
 size_t fast_wave_bytes() { return (size_t)kStageBytes; }

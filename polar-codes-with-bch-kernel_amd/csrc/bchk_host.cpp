@@ -405,6 +405,7 @@ struct bchk_ctx {
     // latency-bound search / tail kernels.
     struct Pipe {
         DevBuf queue, heavy, ctrl, l1q, l1rec;  // l1q / l1rec: first pass -> analytic tail
+        DevBuf pre;                             // m >= 7: the lane pre-pass's finished rows
         hipStream_t s = nullptr, aux = nullptr;  // s unused for pipe 0 (the caller's stream)
         hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_done = nullptr, ev_fast = nullptr;
     };
@@ -435,6 +436,9 @@ struct bchk_ctx {
     // fast ring kernel: waves per workgroup (BCHK_FAST_RING_WAVES, 0 = 16) and experiment
     // mode (BCHK_FAST_MODE)
     uint32_t fast_waves = 0, fast_mode = 0;
+    // m >= 7: the lane-per-codeword pre-pass of the first kernel (BCHK_LANE_PRE=0: off)
+    FastFn lane = nullptr;
+    bool lane_pre = true;
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
     // hybrid tail: a first-pass hand-off whose loop bound is below this goes to a cooperative
@@ -518,6 +522,7 @@ void release_pipes(bchk_ctx *c) {
         P.ctrl.release();
         P.l1q.release();
         P.l1rec.release();
+        P.pre.release();
         if (P.s) (void)hipStreamDestroy(P.s);
         if (P.aux) (void)hipStreamDestroy(P.aux);
         for (hipEvent_t e : {P.ev_fork, P.ev_join, P.ev_done, P.ev_fast})
@@ -567,6 +572,9 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
     if ((rc = P.ctrl.ensure(kCtrlBytes)) || (rc = ensure_heavy(P, B, s))) return rc;
     const bool fast = c->fast && c->use_fast;
     if (fast && (rc = P.queue.ensure(B * sizeof(uint32_t)))) return rc;
+    // the pre-pass decides rows without a stats record (the first kernel writes those)
+    const bool lane = fast && c->lane && c->lane_pre && !d_st;
+    if (lane && (rc = P.pre.ensure((B + 63) / 64 * sizeof(uint64_t)))) return rc;
     uint32_t *ctrl = (uint32_t *)P.ctrl.p;
     SearchParams p{};
     p.y = d_y;
@@ -650,6 +658,10 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
         if (c->m <= 6) {
             f.fast_waves = c->fast_waves;
             f.fast_mode = c->fast_mode;
+        }
+        if (lane) {
+            f.pre_mask = (uint64_t *)P.pre.p;
+            HIP_TRY(c->lane(f, 0, s));
         }
         HIP_TRY(c->fast(f, c->lds_fast, s));
     }
@@ -873,6 +885,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     c->lds_alg = tb;
     if (select_fast(m, t, &c->fast))  // m >= 7: kaneko_first_kernel, the search kernel's layout
         c->lds_fast = m >= 7 ? c->lds : tb + fast_block_waves() * fast_wave_bytes();
+    if (m >= 7 && !select_lane(m, t, &c->lane)) c->lane = nullptr;
+    if (const char *lp = getenv("BCHK_LANE_PRE")) c->lane_pre = atoi(lp) != 0;
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     if (getenv("BCHK_NO_TABLE")) c->use_table = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);

@@ -209,6 +209,12 @@ kaneko_first_kernel(SearchParams p) {
     if (cw0 >= p.count) return;
     const uint32_t nrows = p.count - cw0 < kFirstPerWave ? p.count - cw0 : kFirstPerWave;
     const uint32_t nbytes = nrows * (uint32_t)N;
+    // rows the lane pre-pass finished (kaneko_lane_kernel) are not touched
+    static_assert(64 % kFirstPerWave == 0, "a wave's rows lie in one pre_mask word");
+    const uint32_t rmask = (1u << nrows) - 1u;
+    const uint32_t skip = p.pre_mask ? (uint32_t)(p.pre_mask[cw0 >> 6] >> (cw0 & 63u)) & rmask : 0u;
+    if (skip == rmask) return;
+    const uint32_t todo = rmask & ~skip;
     // 8-B pieces: row blocks start at a multiple of 8 rows (8 N bytes); the tail of a ragged
     // last block byte by byte
     const bool wide = nrows == kFirstPerWave && ((reinterpret_cast<uintptr_t>(p.tx) | reinterpret_cast<uintptr_t>(p.res)) & 7u) == 0;
@@ -225,20 +231,24 @@ kaneko_first_kernel(SearchParams p) {
     // (and its sent word, for the fused counters at the output step, with a stats record)
     double ynext[NW];
     TxPre<NW> txnext{{}, false};
-    load_row<M>(p, cw0, lane, ynext);
-    if (!SEL) txnext = tx_prefetch<M>(p, cw0, lane);
+    const uint32_t kfirst = (uint32_t)__builtin_ctz(todo);
+    load_row<M>(p, cw0 + kfirst, lane, ynext);
+    if (!SEL) txnext = tx_prefetch<M>(p, cw0 + kfirst, lane);
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
     uint32_t fin = 0;     // SEL: rows finished here (bit k: codeword cw0 + k)
     double l0k = 0.0;     // SEL: lane k holds codeword cw0 + k's l0
-    for (uint32_t k = 0; k < nrows; ++k) {
+    for (uint32_t k = kfirst; k < nrows; ++k) {
+        if (!((todo >> k) & 1u)) continue;
         const uint32_t cw = cw0 + k;
         double yv[NW];
 #pragma unroll
         for (int s = 0; s < NW; ++s) yv[s] = ynext[s];
         const TxPre<NW> txp = txnext;
-        if (k + 1 < nrows) {
-            load_row<M>(p, cw + 1, lane, ynext);
-            if (!SEL) txnext = tx_prefetch<M>(p, cw + 1, lane);
+        const uint32_t rest = todo & ~((2u << k) - 1u);  // the next row to decode
+        if (rest) {
+            const uint32_t kn = (uint32_t)__builtin_ctz(rest);
+            load_row<M>(p, cw0 + kn, lane, ynext);
+            if (!SEL) txnext = tx_prefetch<M>(p, cw0 + kn, lane);
         }
 #if defined(BCHK_FIRST_CUT) && BCHK_FIRST_CUT == 1
         // experiment builds only (wrong results, timing of the phases): channel loads
@@ -246,16 +256,18 @@ kaneko_first_kernel(SearchParams p) {
         continue;
 #endif
         if constexpr (TMAX <= 15) {
-            if ((k & 3u) == 0) {
-                // test pattern 0 of this and the next three words: one four-row key-equation
-                // solve (their rows are read again, from the cache, for the prep)
+            const uint32_t kb = k & ~3u;
+            if (k == (uint32_t)__builtin_ctz(todo & (0xFu << kb))) {
+                // test pattern 0 of the four words of this row's group (its first row to
+                // decode): one four-row key-equation solve (their rows are read again, from
+                // the cache, for the prep)
                 constexpr int W = Prep<M, TMAX>::W;
                 uint32_t *s4s = reinterpret_cast<uint32_t *>(e4s + 5 * NW);  // [4][W]
 #pragma nounroll
                 for (int q = 0; q < 4; ++q) {  // one row at a time (registers)
                     uint32_t Sq[W];
-                    if (k + (uint32_t)q < nrows) {
-                        hard_syndromes<M, TMAX>(p, col, cw + (uint32_t)q, lane, Sq);
+                    if (((todo >> (kb + (uint32_t)q)) & 1u) != 0u) {
+                        hard_syndromes<M, TMAX>(p, col, cw0 + kb + (uint32_t)q, lane, Sq);
                     } else {
 #pragma unroll
                         for (int w = 0; w < W; ++w) Sq[w] = 0;

@@ -39,6 +39,8 @@ typedef hipError_t (*FastFn)(const SearchParams &, size_t, hipStream_t);
 // codeword for m >= 7 (kaneko_first_kernel, bchk_kernels.hip); false when (m, t) has none.
 bool select_fast(int m, int t, FastFn *out);
 bool select_first_long(int m, int t, FastFn *out);
+// the lane pre-pass of the long-code first kernel (m >= 7, t <= 15; false: none)
+bool select_lane(int m, int t, FastFn *out);
 size_t fast_wave_bytes();
 int fast_block_waves();  // waves per block of the fast kernel
 

@@ -721,3 +721,57 @@ def test_long_code_dense_redecode_handshake(long_rec):
         print(f"\nlong_rec {long_rec}: {started} cooperative codewords, {served} dense re-decodes")
     finally:
         d.close()
+
+
+def _decode_count(d, y, tx, fill):
+    import torch
+    B = y.shape[0]
+    dy, dtx = torch.from_numpy(y).cuda(), torch.from_numpy(tx).cuda()
+    dres = torch.from_numpy(fill.copy()).cuda()
+    dl0 = torch.zeros(B, dtype=torch.float64, device="cuda")
+    c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    d.decode_count_device(dy.data_ptr(), dtx.data_ptr(), B, dres.data_ptr(), dl0.data_ptr(), 0, c6.data_ptr())
+    d.sync()
+    return dres.cpu().numpy(), dl0.cpu().numpy(), c6.cpu().numpy()
+
+
+@pytest.mark.parametrize("m,t,J,snr", [(8, 15, 15, 5.0), (8, 15, 15, 7.0), (8, 15, -1, 6.0), (7, 8, 15, 5.0),
+                                       (7, 6, -1, 7.0)])
+def test_lane_prepass_equals_first_kernel(m, t, J, snr):
+    # m >= 7 without a stats record: the lane-per-codeword pre-pass (kaneko_lane_kernel)
+    # decides the rows that return at test pattern 0 or 1 and the first kernel skips them.
+    # Decoded rows, l0 bits and the fused counters equal a context without the pre-pass,
+    # on a ragged batch (partial last chunk) with edge rows (exact and prefix ties, tiny,
+    # huge and zero samples, a noiseless codeword) and rows never accepted (the caller's fill)
+    on = dec(m, t, J=J)
+    off = _ctx_env(m, t, J, BCHK_LANE_PRE=0)
+    try:
+        B = (1 << 14) + 37
+        tx, y, _ = on.generate(snr, B, seed=71)
+        y = y.copy()
+        n = on.n
+        y[0, 5] = -y[0, 9]
+        y[64, 3] = np.nextafter(y[64, 8], np.inf if y[64, 8] > 0 else -np.inf)
+        y[65, 7] = 1e-300
+        y[66, 7] = 1e300
+        y[67, 11] = 0.0
+        y[68, :] = np.where(tx[68] == 1, 1.0, -1.0)
+        y[B - 1, n - 1] = -y[B - 1, 0] * (1 + 2.0 ** -50)
+        y[130, 2] = -y[130, 2] * 2.0 ** -40              # tiny |y| at one position
+        fill = (np.arange(B * n, dtype=np.uint64).reshape(B, n) % 3 == 0).astype(np.uint8)
+        a = _decode_count(on, y, tx, fill)
+        b = _decode_count(off, y, tx, fill)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+        np.testing.assert_array_equal(a[2], b[2])
+        if J < 0:
+            return  # (uncapped rows can take the CPU oracle minutes: J = 15 cases below)
+        # and a sample of plain rows against the oracle
+        idx = np.random.default_rng(7).choice(np.arange(256, B - 64), 48, replace=False)
+        r2, l2, s2, a2 = Oracle(m, t).kaneko_batch(y[idx], J=J)
+        acc = a2.astype(bool)
+        np.testing.assert_array_equal(a[0][idx][acc], r2[acc])
+        np.testing.assert_array_equal(a[1][idx][acc].view(np.uint64), l2[acc].view(np.uint64))
+    finally:
+        off.close()
