@@ -73,6 +73,9 @@ struct SearchParams {
     // long codes (m >= 7): the lane pre-pass (kaneko_lane_kernel) sets bit k of word c when
     // it finished codeword 64 c + k; kaneko_first_kernel skips those (null: no pre-pass)
     uint64_t *pre_mask;
+    // its hard-decision syndrome table: [ceil(n/8)][256][W] words, entry (j, v) = the
+    // syndrome of byte value v at positions 8j .. 8j + 7
+    const uint32_t *syn8;
     // heavy codewords: the wave kernel hands a codeword still running after chunk_limit
     // steps of 64 patterns to the cooperative kernel, which may run concurrently with it
     // (heavy_tail == null disables the hand-off). Longest-first: codewords whose loop bound

@@ -936,9 +936,10 @@ static hipError_t launch_fast_impl(const SearchParams &p, size_t lds, hipStream_
 //     (alg_decode_lanes: binary BM, split test, wave-spread Chien scan of each success).
 constexpr int kLaneWaves = 8;                   // waves per workgroup (2 workgroups per CU)
 constexpr int kLaneSeg = 16;                    // positions per staged segment
-constexpr int kLaneRowD = kLaneSeg + 1;         // doubles per staged row (pad: b64 reads spread)
-constexpr int kLaneWaveBytes = 64 * kLaneRowD * 8;
+constexpr int kLaneRowD = kLaneSeg + 1;         // hi words per staged row (pad: conflict-free reads)
 constexpr int kLaneKeep = 32;
+// the row buffer (64 x kLaneRowD hi words), then the parked keys (64 x 33), then the masks
+constexpr int kLaneWaveBytes = 64 * (kLaneKeep + 1) * 4;
 
 // 24-bit prefix (5 exponent bits, 19 mantissa bits; 0: |y| < 2^-27 or zero, all ones:
 // |y| >= 32, inf, NaN) above the 8-bit position
@@ -986,10 +987,148 @@ __device__ __forceinline__ bool mask_bit(const Mask<NW> &m, int pos) {
     return b & 1u;
 }
 
+// Decoder::decode (src/Decoder.cpp:298-321) of one word per lane for the pre-pass, where
+// nearly every lane succeeds: binary BM (bm_locator); the roots of a locator of degree 1
+// (1 + C1 x: x = 1/C1) and 2 (1 + C1 x + C2 x^2 = 0 with x = (C1/C2) z: z^2 + z = C2/C1^2,
+// solved by the table quad[c] = a root z, 0 when there is none; C1 = 0 is a double root)
+// in closed form, degree 3 too (below); degree >= 4 by the wave-spread Chien scan of
+// alg_decode_lanes_g, one scan per such lane. Success and flipped positions as alg_core's (a root alpha^k flips
+// position (n - k) mod n, :287): L <= t, deg >= 1 distinct roots in GF(2^m)*.
+template <int M, int TMAX>
+__device__ __forceinline__ bool lane_alg_decode(const uint8_t *ex, const uint16_t *lg, const uint8_t *quad,
+                                                const uint32_t *cub, const uint32_t *Sw, int t, Mask<Geo<M>::NW> &E,
+                                                bool act) {
+    constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
+    const int lane = (int)__lane_id();
+    uint32_t C[TMAX + 1];
+    int L;
+    bm_locator<M, TMAX>(ex, lg, Sw, t, C, L);
+    int deg = 0;
+#pragma unroll
+    for (int i = 1; i <= TMAX; ++i) deg = C[i] ? i : deg;
+    bool ok = act && (L <= t) && (deg >= 1);
+#pragma unroll
+    for (int s = 0; s < NW; ++s) E.w[s] = 0;
+    auto pos_of = [&](int k) { return k ? N - k : 0; };  // root alpha^k, k in [0, n)
+    if (ok && deg == 1) {
+        const int l1 = lg[C[1]];
+        mask_set<NW>(E, pos_of(l1 ? N - l1 : 0));  // x = 1 / C1
+    } else if (ok && deg == 2) {
+        if (C[1] == 0u) {
+            ok = false;
+        } else {
+            const int l1 = lg[C[1]], l2 = lg[C[2]];
+            int lc = l2 - 2 * l1;
+            lc += lc < 0 ? N : 0;
+            lc += lc < 0 ? N : 0;
+            const uint32_t z0 = quad[ex[lc]];
+            if (z0 == 0u) {
+                ok = false;
+            } else {
+                int base = l1 - l2;
+                base += base < 0 ? N : 0;
+                int k0 = base + lg[z0], k1 = base + lg[z0 ^ 1u];
+                k0 -= k0 >= N ? N : 0;
+                k1 -= k1 >= N ? N : 0;
+                mask_set<NW>(E, pos_of(k0));
+                mask_set<NW>(E, pos_of(k1));
+            }
+        }
+    } else if (ok && deg == 3) {
+        // sigma(X) = X^3 + a X^2 + b X + c (X = 1/x, the error locators): X = Y + a gives
+        // Y^3 + p Y + q with p = a^2 + b, q = a b + c; q = 0: a double root; p = 0: Y^3 = q
+        // (three roots iff 3 | n and q is a cube); else Y = sqrt(p) W, W^3 + W = q / p^(3/2)
+        // (cub[r]: its roots, three or fewer)
+        const uint32_t a = C[1], b = C[2], c = C[3];
+        const int la = lg[a], lb = lg[b];
+        const uint32_t P = (a ? (uint32_t)ex[2 * la] : 0u) ^ b;
+        const uint32_t Q = (a && b ? (uint32_t)ex[la + lb] : 0u) ^ c;
+        uint32_t Y0 = 0, Y1 = 0, Y2 = 0;
+        bool three = false;
+        if (Q != 0u) {
+            const int lq = lg[Q];
+            if (P == 0u) {
+                if constexpr (N % 3 == 0) {
+                    if (lq % 3 == 0) {
+                        const int c3 = lq / 3;
+                        Y0 = ex[c3];
+                        Y1 = ex[c3 + N / 3];
+                        Y2 = ex[c3 + 2 * (N / 3)];
+                        three = true;
+                    }
+                }
+            } else {
+                const int lp = lg[P];
+                const int ls = (lp & 1) ? (lp + N) >> 1 : lp >> 1;  // log sqrt(p)
+                int lr = lq - 3 * ls;
+                lr += lr < 0 ? N : 0;
+                lr += lr < 0 ? N : 0;
+                lr += lr < 0 ? N : 0;
+                const uint32_t e3 = cub[ex[lr]];
+                if ((e3 >> 24) == 3u) {
+                    const uint32_t w0 = e3 & 255u, w1 = (e3 >> 8) & 255u, w2 = (e3 >> 16) & 255u;
+                    Y0 = w0 ? ex[lg[w0] + ls] : 0u;
+                    Y1 = w1 ? ex[lg[w1] + ls] : 0u;
+                    Y2 = w2 ? ex[lg[w2] + ls] : 0u;
+                    three = true;
+                }
+            }
+        }
+        const uint32_t X0 = Y0 ^ a, X1 = Y1 ^ a, X2 = Y2 ^ a;
+        if (!three || !X0 || !X1 || !X2) {
+            ok = false;
+        } else {
+            mask_set<NW>(E, lg[X0]);
+            mask_set<NW>(E, lg[X1]);
+            mask_set<NW>(E, lg[X2]);
+        }
+    }
+    const bool scan = ok && deg >= 4;
+    int lc[TMAX + 1];
+#pragma unroll
+    for (int i = 0; i <= TMAX; ++i) lc[i] = lg[C[i]];
+    for (uint64_t sm = ballot(scan); sm; sm &= sm - 1) {
+        const int src = (int)__builtin_ctzll(sm);
+        const int dg = uni(__shfl(deg, src, 64));
+        int kk[NW], ik[NW];
+        uint32_t v[NW];
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            const int pos = lane + 64 * s;
+            kk[s] = pos ? N - pos : 0;
+            ik[s] = 0;
+            v[s] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i <= TMAX; ++i) {
+            if (i <= dg) {
+                const int lti = __builtin_amdgcn_readlane(lc[i], src);
+#pragma unroll
+                for (int s = 0; s < NW; ++s) {
+                    v[s] ^= gf_exp2<M>(ex, lti, ik[s]);
+                    ik[s] += kk[s];
+                    ik[s] = ik[s] >= N ? ik[s] - N : ik[s];
+                }
+            }
+        }
+        int cnt = 0;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            const uint64_t r = ballot(lane + 64 * s < N && v[s] == 0u);
+            cnt += __popcll(r);
+            if (lane == src) E.w[s] = r;
+        }
+        if (lane == src && cnt != dg) ok = false;
+    }
+    return ok;
+}
+
 // fast_decide for n <= 255 (NW words): the same exits, tests and bounds from k[0..KMAX+1]
+// (k: the lane's kept keys, parked in LDS while the decoders hold their registers)
 template <int M, int TMAX>
 __device__ __forceinline__ LaneRes<Geo<M>::NW> lane_decide(const uint8_t *ex, const uint16_t *lg, const uint32_t *col,
-                                                           const uint32_t (&k)[kLaneKeep], uint32_t kmax_real,
+                                                           const uint8_t *quad, const uint32_t *cub,
+                                                           const uint32_t *syn8, const uint32_t *k, uint32_t kmax_real,
                                                            const Mask<Geo<M>::NW> &yH, const double *yrow, bool live,
                                                            int t, double s2) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
@@ -1000,26 +1139,25 @@ __device__ __forceinline__ LaneRes<Geo<M>::NW> lane_decide(const uint8_t *ex, co
     bool bad = (k[0] >> 8) == 0u || (kmax_real >> 8) == 0xFFFFFFu;
 #pragma unroll
     for (int r = 0; r < KMAX + 1; ++r) bad |= ((k[r] ^ k[r + 1]) >> 8) == 0u;
-    uint32_t pre[NPF];
-#pragma unroll
-    for (int r = 0; r < NPF; ++r) pre[r] = k[r];
+    const uint32_t *pre = k;
     const int o0 = (int)(k[0] & 255u);
     const double c2 = 2.0 / s2;
-    // syndrome of the hard decision (Decoder::findSyndromPoly :184-207): uniform positions,
-    // broadcast column reads
+    // syndrome of the hard decision (Decoder::findSyndromPoly :184-207): the XOR of the
+    // byte table's entries (syn8[j][v] = the syndrome of byte value v at positions 8j ..
+    // 8j + 7; L2-resident, one 16-B load per byte of the row)
     uint32_t S0[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) S0[w] = 0;
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
-        const uint32_t lo32 = (uint32_t)yH.w[s], hi32 = (uint32_t)(yH.w[s] >> 32);
-#pragma unroll 8
-        for (int b = 0; b < 64; ++b) {
-            const int pos = 64 * s + b;
-            if (pos < N) {
-                const uint32_t on = (uint32_t)((int32_t)((b < 32 ? lo32 << (31 - b) : hi32 << (63 - b))) >> 31);
 #pragma unroll
-                for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w] & on;
+        for (int b = 0; b < 8; ++b) {
+            const int j = 8 * s + b;
+            if (8 * j < N) {
+                const uint32_t v = (uint32_t)(yH.w[s] >> (8 * b)) & 255u;
+                const uint32_t *e = syn8 + ((size_t)j * 256 + v) * W;
+#pragma unroll
+                for (int w = 0; w < W; ++w) S0[w] ^= e[w];
             }
         }
     }
@@ -1071,7 +1209,7 @@ __device__ __forceinline__ LaneRes<Geo<M>::NW> lane_decide(const uint8_t *ex, co
 #pragma unroll
     for (int w = 0; w < W; ++w) zero0 = zero0 && S0[w] == 0u;
     Mask<NW> E;
-    const bool ok0 = alg_decode_lanes<M, TMAX>(ex, lg, S0, t, E, live && !bad && !zero0);
+    const bool ok0 = lane_alg_decode<M, TMAX>(ex, lg, quad, cub, S0, t, E, live && !bad && !zero0);
     if (live && !bad && ok0) {
         double l;
         bool ret;
@@ -1094,7 +1232,7 @@ __device__ __forceinline__ LaneRes<Geo<M>::NW> lane_decide(const uint8_t *ex, co
         uint32_t S1[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) S1[w] = S0[w] ^ col[o0 * W + w];
-        const bool ok1 = alg_decode_lanes<M, TMAX>(ex, lg, S1, t, E, need1);
+        const bool ok1 = lane_alg_decode<M, TMAX>(ex, lg, quad, cub, S1, t, E, need1);
         if (need1 && ok1) {
             Mask<NW> diff = E;
 #pragma unroll
@@ -1109,35 +1247,63 @@ __device__ __forceinline__ LaneRes<Geo<M>::NW> lane_decide(const uint8_t *ex, co
 }
 
 template <int M, int TMAX>
-__global__ void __launch_bounds__(kWaveSize * kLaneWaves) kaneko_lane_kernel(SearchParams p) {
+#ifndef BCHK_LANE_WPE
+#define BCHK_LANE_WPE 4  // waves per SIMD (two workgroups per CU; LDS allows four)
+#endif
+__global__ void __launch_bounds__(kWaveSize * kLaneWaves) __attribute__((amdgpu_waves_per_eu(BCHK_LANE_WPE, BCHK_LANE_WPE)))
+kaneko_lane_kernel(SearchParams p) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
     constexpr int NSEG = (N + kLaneSeg - 1) / kLaneSeg;
     static_assert(kLaneSeg == 16, "segment = four rows of 16 positions per wave instruction");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
+    const uint32_t tb = (p.td.bytes + 15) & ~15u;
+    uint32_t *cub = reinterpret_cast<uint32_t *>(smem + tb);  // [2^m]: roots of W^3 + W = r
+    uint8_t *quad = smem + tb + 4 * (1 << M);  // [2^m]: a root z of z^2 + z = c, 0 when there is none
+    for (int c = threadIdx.x; c < (1 << M); c += blockDim.x) {
+        quad[c] = 0;
+        cub[c] = 0;
+    }
     __syncthreads();
     const uint8_t *ex = smem + p.td.off_exp;
     const uint16_t *lg = reinterpret_cast<const uint16_t *>(smem + p.td.off_log);
     const uint32_t *col = reinterpret_cast<const uint32_t *>(smem + p.td.off_col);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint8_t *wb = smem + ((p.td.bytes + 15) & ~15u) + wid * kLaneWaveBytes;
-    double *seg = reinterpret_cast<double *>(wb);
+    for (int z = threadIdx.x; z < (1 << M); z += blockDim.x) {
+        // c = z^2 + z; z and z + 1 give the same c (either root serves)
+        const uint32_t z2 = z ? ex[2 * lg[z]] : 0u;
+        if (z != 1) quad[z2 ^ (uint32_t)z] = (uint8_t)z;
+        // r = z^3 + z: up to three roots (bytes 0..2) and their count (byte 3)
+        int l3 = z ? 3 * lg[z] : 0;  // the exp table is zero from 2n - 1 on: reduce mod n
+        l3 -= l3 >= Geo<M>::N ? Geo<M>::N : 0;
+        l3 -= l3 >= Geo<M>::N ? Geo<M>::N : 0;
+        const uint32_t z3 = z ? ex[l3] : 0u;
+        const uint32_t r = z3 ^ (uint32_t)z;
+        const uint32_t old = atomicAdd(&cub[r], 1u << 24) >> 24;
+        if (old < 3u) atomicOr(&cub[r], (uint32_t)z << (8 * old));
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = uni((int)(threadIdx.x >> 6));  // wave-uniform: SGPRs
+    uint8_t *wb = smem + tb + 5 * (1 << M) + wid * kLaneWaveBytes;
+    uint32_t *seg = reinterpret_cast<uint32_t *>(wb);  // hi words, [64][kLaneRowD]
     const uint32_t gk = blockIdx.x * kLaneWaves + (uint32_t)wid;  // this wave's chunk
     const uint32_t nch = (p.count + 63u) / 64u;
     if (gk >= nch) return;
     const uint32_t cw0 = 64u * gk, cw = cw0 + (uint32_t)lane;
     const bool live = cw < p.count;
     const uint32_t rows = p.count - cw0 < 64u ? p.count - cw0 : 64u;
-    // segment loads: instruction i, lane l -> row 4 i + l / 16, position 16 g + l % 16
+    // segment loads: instruction i, lane l -> row 4 i + l / 16, position 16 g + l % 16, as
+    // buffer loads over the chunk's rows (one lane offset, the row group in the scalar
+    // offset; rows past the batch read 0, position n -- the next row's first -- is unused)
     const int lr = lane >> 4, lj = lane & 15;
-    double pf[16];
+    const __amdgpu_buffer_rsrc_t ysrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(p.y + (size_t)cw0 * N), (short)0, (int)(rows * (uint32_t)N * 8u), 0x00020000);
+    // (the keys and the hard decision need the hi words only: half the registers and LDS;
+    // the acceptance tests read exact values from the rows again)
+    uint32_t pf[16];
     auto load_seg = [&](int g) {
-        const int pos = kLaneSeg * g + lj;
+        const int voff = (lr * N + kLaneSeg * g + lj) * 8 + 4;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t r = 4u * i + (uint32_t)lr;
-            pf[i] = (pos < N && r < rows) ? p.y[(size_t)(cw0 + r) * N + pos] : 0.0;
-        }
+        for (int i = 0; i < 16; ++i) pf[i] = __builtin_amdgcn_raw_buffer_load_b32(ysrc, voff, i * 4 * N * 8, 0);
     };
     load_seg(0);
     uint32_t kept[kLaneKeep];
@@ -1159,8 +1325,7 @@ __global__ void __launch_bounds__(kWaveSize * kLaneWaves) kaneko_lane_kernel(Sea
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int pos = kLaneSeg * g + i;
-            const uint64_t bb = (uint64_t)__double_as_longlong(seg[lane * kLaneRowD + i]);
-            const uint32_t hi = (uint32_t)(bb >> 32);
+            const uint32_t hi = seg[lane * kLaneRowD + i];
             nk[i] = pos < N ? sort_key8(hi, pos) : 0xFFFFFFFFu;
             sb |= (pos < N ? (~hi >> 31) : 0u) << i;
         }
@@ -1177,11 +1342,17 @@ __global__ void __launch_bounds__(kWaveSize * kLaneWaves) kaneko_lane_kernel(Sea
         for (int s = 0; s < NW; ++s)
             yH.w[s] |= (g >> 2) == s ? (uint64_t)sb << (16 * (g & 3)) : 0ull;
     }
+    // the kept keys into the (now free) row buffer, lane-major with stride 33 (conflict-free)
+    wave_sync();
+    static_assert(64 * (kLaneKeep + 1) * 4 <= kLaneWaveBytes, "the parked keys fit the row buffer");
+    uint32_t *kl = reinterpret_cast<uint32_t *>(wb) + lane * (kLaneKeep + 1);
+#pragma unroll
+    for (int i = 0; i < kLaneKeep; ++i) kl[i] = kept[i];
     int t = p.t;
     double s2 = p.s2;
     asm volatile("" : "+s"(t), "+s"(s2));
     const double *yrow = p.y + (size_t)(live ? cw : cw0) * N;
-    const LaneRes<NW> R = lane_decide<M, TMAX>(ex, lg, col, kept, kmax_real, yH, yrow, live, t, s2);
+    const LaneRes<NW> R = lane_decide<M, TMAX>(ex, lg, col, quad, cub, p.syn8, kl, kmax_real, yH, yrow, live, t, s2);
 
     // ---- outputs: decoded rows of the finished codewords (others untouched: the first
     // kernel writes them), their l0, the fused counters and the chunk's pre_mask word
@@ -1257,7 +1428,7 @@ template <int M, int TMAX>
 static hipError_t launch_lane_impl(const SearchParams &p, size_t, hipStream_t s) {
     const uint32_t chunks = (p.count + 63u) / 64u;
     const int blocks = (int)((chunks + kLaneWaves - 1) / kLaneWaves);
-    const size_t lds = ((p.td.bytes + 15) & ~size_t(15)) + (size_t)kLaneWaves * kLaneWaveBytes;
+    const size_t lds = ((p.td.bytes + 15) & ~size_t(15)) + 5 * (1u << M) + (size_t)kLaneWaves * kLaneWaveBytes;
     static bool attr = false;
     if (!attr && lds > 65536) {
         (void)hipFuncSetAttribute((const void *)&kaneko_lane_kernel<M, TMAX>,

@@ -439,6 +439,7 @@ struct bchk_ctx {
     // m >= 7: the lane-per-codeword pre-pass of the first kernel (BCHK_LANE_PRE=0: off)
     FastFn lane = nullptr;
     bool lane_pre = true;
+    DevBuf syn8;  // its hard-decision syndrome table (SearchParams::syn8)
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
     // hybrid tail: a first-pass hand-off whose loop bound is below this goes to a cooperative
@@ -661,6 +662,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
         }
         if (lane) {
             f.pre_mask = (uint64_t *)P.pre.p;
+            f.syn8 = (const uint32_t *)c->syn8.p;
             HIP_TRY(c->lane(f, 0, s));
         }
         HIP_TRY(c->fast(f, c->lds_fast, s));
@@ -886,6 +888,22 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (select_fast(m, t, &c->fast))  // m >= 7: kaneko_first_kernel, the search kernel's layout
         c->lds_fast = m >= 7 ? c->lds : tb + fast_block_waves() * fast_wave_bytes();
     if (m >= 7 && !select_lane(m, t, &c->lane)) c->lane = nullptr;
+    if (c->lane) {
+        // the pre-pass's byte syndrome table from the column table (same word stride W)
+        const int n = c->field.n, W = (int)c->td.W, NB = (n + 7) / 8;
+        const uint32_t *colh = reinterpret_cast<const uint32_t *>(c->tables_host.data() + c->td.off_col);
+        std::vector<uint32_t> syn((size_t)NB * 256 * W, 0u);
+        for (int j = 0; j < NB; ++j)
+            for (int v = 0; v < 256; ++v)
+                for (int b = 0; b < 8; ++b)
+                    if (((v >> b) & 1) && 8 * j + b < n)
+                        for (int w = 0; w < W; ++w) syn[((size_t)j * 256 + v) * W + w] ^= colh[(8 * j + b) * W + w];
+        if (c->syn8.ensure(syn.size() * 4) != 0 ||
+            hipMemcpy(c->syn8.p, syn.data(), syn.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            bchk_destroy(c);
+            return fail(BCHK_EHIP, "device setup failed: %s", hipGetErrorString(hipGetLastError()));
+        }
+    }
     if (const char *lp = getenv("BCHK_LANE_PRE")) c->lane_pre = atoi(lp) != 0;
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     if (getenv("BCHK_NO_TABLE")) c->use_table = false;
@@ -952,6 +970,7 @@ void bchk_destroy(bchk_ctx *c) {
     c->words.release();
     c->synd.release();
     c->ok.release();
+    c->syn8.release();
     if (c->d_tables) (void)hipFree(c->d_tables);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
