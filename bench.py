@@ -287,11 +287,17 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
     # n <= 63: the ring kernel serves calls without a stats record where the 16-key selection
     # covers the decision (csrc/bchk_fast.hip launch_fast_impl), else the staged kernel
     ring = (min(2 * tm, n - 1) + 2 <= 16 and not args.unfused and os.environ.get("BCHK_FAST_RING", "1") != "0")
-    fast_name = ("kaneko_fast_ring_kernel" if ring else "kaneko_fast_kernel") if args.m <= 6 else "kaneko_first_kernel"
+    # n > 63, t <= 15 (m = 7: TMAX 8): the lane pre-pass decides the rows that return at test
+    # pattern 0 or 1, the first kernel the others (stage 0 = both launches)
+    lane = (args.m == 8 and tm <= 15) or (args.m == 7 and tm <= 8)
+    lane = lane and os.environ.get("BCHK_LANE_PRE", "1") != "0"
+    tsuf = f"<{args.m},{tm}>"
+    fast_name = (("kaneko_fast_ring_kernel" if ring else "kaneko_fast_kernel") + tsuf if args.m <= 6
+                 else (f"kaneko_lane_kernel{tsuf} + kaneko_first_kernel{tsuf}" if lane else "kaneko_first_kernel" + tsuf))
     fast_on = has_fast and ms4[0] > 0 and n_exact < B
     # per launch: average duration (HIP events on the launching stream) and the codewords
     # one launch processes
-    kern = [{"name": f"{fast_name}<{args.m},{tm}>" if has_fast else "control memset",
+    kern = [{"name": fast_name if has_fast else "control memset",
              "ms": ms4[0] / launches, "codewords": B if has_fast else 0},
             {"name": f"kaneko_search_kernel<{args.m},{tm}>", "ms": ms4[1] / launches,
              "codewords": n_exact if fast_on else B},
@@ -351,15 +357,20 @@ def main():
     head = pts[args.snr]
     dom = next(k for k in head["kernels"] if k["name"] == head["dominant_kernel"])
     # HBM bytes per launch of the dominant kernel, from the committed PMC passes of the same
-    # workload (scripts/gpu_final.sh -> scripts/traffic_json.py, rocprofv3 --pmc FETCH_SIZE
-    # x 2 (gfx950) + WRITE_SIZE); null when no profile of this workload exists. It is a
-    # stored measurement (rocprofv3 cannot run inside this process): its source is named.
-    traffic, traffic_src = None, None
+    # workload (scripts/gpu_final5.sh -> scripts/traffic_req_json.py, rocprofv3 --pmc memory-
+    # side requests by size); null when no profile of this workload exists. It is a stored
+    # measurement (rocprofv3 cannot run inside this process): its source is named. A stage of
+    # two launches (lane pre-pass + first kernel) sums both.
+    traffic, traffic_src, traffic_read = None, None, None
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
             if tr.get("batch") == B and tr.get("snr_db") == args.snr and tr.get("J") == args.J:
-                traffic = tr.get("kernels", {}).get(dom["name"].replace(" ", ""))
+                names = [k.replace(" ", "") for k in dom["name"].split(" + ")]
+                parts = [tr.get("kernels", {}).get(k) for k in names]
+                traffic = None if any(v is None for v in parts) else sum(parts)
+                rparts = [tr.get("read_bytes", {}).get(k) for k in names]
+                traffic_read = None if any(v is None for v in rparts) else sum(rparts)
                 traffic_src = f"{tr.get('source')} ({tr.get('date', 'undated')})"
         except Exception:
             traffic = None
@@ -394,6 +405,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(head["dominant_GB_s"], 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(head["frac"], 6), "traffic": traffic,
                          "traffic_source": traffic_src,
+                         # its HBM reads against the inputs it streams: the rows (8n B per
+                         # codeword) and, in the fused step, the sent words (n B)
+                         "traffic_read": traffic_read,
+                         "read_over_inputs": (round(traffic_read / ((8.0 * n + (0 if args.unfused else n)) * B), 4)
+                                              if traffic_read else None),
                          "bytes_per_codeword": head["bytes_per_codeword"],
                          "achieved_fused": round(head["dominant_GB_s_fused"], 3),
                          "frac_fused": round(head["dominant_GB_s_fused"] / HBM_PEAK_GBS, 6),

@@ -37,8 +37,10 @@ for k in sorted(set(rd) & set(wr)):
     w64 = w.get("TCC_EA0_WRREQ_64B_sum", 0)
     wb = 64 * w64 + 32 * (w.get("TCC_EA0_WRREQ_sum", 0) - w64)
     key = re.sub(r"\s+", "", k)
-    if key.startswith("kaneko_fast_kernel"):  # bench.py's name: without the selection flag
-        key = key.replace(",true>", ">").replace(",false>", ">")
+    # bench.py's names: without the template flags; the search kernel's analytic-tail
+    # instance (its last flag set) named as bench.py names it
+    tail = key.startswith("kaneko_search_kernel") and key.endswith(",true>")
+    key = re.sub(r",(true|false)", "", key) + ("analytictail" if tail else "")
     res["kernels"][key] = round(rb + wb)
     res["read_bytes"][key] = round(rb)
     res["write_bytes"][key] = round(wb)
