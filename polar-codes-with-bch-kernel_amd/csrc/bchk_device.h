@@ -155,6 +155,12 @@ struct SearchParams {
     // [0] dense re-decodes served, [1] heavy codewords started
     int32_t long_rec;
     uint32_t *coop_stats;
+    // cooperative kernel, m >= 7: cross-workgroup help (null: off). Workgroup b's codeword
+    // is job b: its control line (jobctl, 128 B each, zeroed per launch) and its data
+    // (jobs, KernelSet::long_job_bytes each: result tags and records, the prep tables).
+    // Workgroups left without a heavy codeword decode chunks of the published ones.
+    void *long_jobctl;
+    void *long_jobs;
 };
 constexpr int kCntSlots = 512;
 constexpr int kCntStride = 16;  // u64 per slot: one 128-B line

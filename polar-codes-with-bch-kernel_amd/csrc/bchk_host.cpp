@@ -406,6 +406,7 @@ struct bchk_ctx {
     struct Pipe {
         DevBuf queue, heavy, ctrl, l1q, l1rec;  // l1q / l1rec: first pass -> analytic tail
         DevBuf pre;                             // m >= 7: the lane pre-pass's finished rows
+        DevBuf jobctl, jobs;                    // m >= 7: cooperative-kernel jobs (help)
         hipStream_t s = nullptr, aux = nullptr;  // s unused for pipe 0 (the caller's stream)
         hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_done = nullptr, ev_fast = nullptr;
     };
@@ -439,6 +440,8 @@ struct bchk_ctx {
     // m >= 7: the lane-per-codeword pre-pass of the first kernel (BCHK_LANE_PRE=0: off)
     FastFn lane = nullptr;
     bool lane_pre = true;
+    // m >= 7: idle cooperative workgroups help the running long codewords (BCHK_LONG_HELP=0: off)
+    bool long_help = true;
     DevBuf syn8;  // its hard-decision syndrome table (SearchParams::syn8)
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
@@ -524,6 +527,8 @@ void release_pipes(bchk_ctx *c) {
         P.l1q.release();
         P.l1rec.release();
         P.pre.release();
+        P.jobctl.release();
+        P.jobs.release();
         if (P.s) (void)hipStreamDestroy(P.s);
         if (P.aux) (void)hipStreamDestroy(P.aux);
         for (hipEvent_t e : {P.ev_fork, P.ev_join, P.ev_done, P.ev_fast})
@@ -770,6 +775,14 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
         HIP_TRY(hipStreamWaitEvent(s, P.ev_join, 0));
     }
     if (p.heavy_tail) {
+        if (c->m >= 7 && c->long_help && c->ks.long_job_bytes) {  // jobs of the cooperative workgroups
+            if ((rc = P.jobctl.ensure((size_t)grid_coop * 128)) ||
+                (rc = P.jobs.ensure((size_t)grid_coop * c->ks.long_job_bytes)))
+                return rc;
+            HIP_TRY(hipMemsetAsync(P.jobctl.p, 0, (size_t)grid_coop * 128, cs));
+            pc.long_jobctl = P.jobctl.p;
+            pc.long_jobs = P.jobs.p;
+        }
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));
         HIP_TRY(launch_coop(c->ks, pc, grid_coop, c->lds_coop, cs));
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[5], cs));
@@ -905,6 +918,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
         }
     }
     if (const char *lp = getenv("BCHK_LANE_PRE")) c->lane_pre = atoi(lp) != 0;
+    if (const char *lh = getenv("BCHK_LONG_HELP")) c->long_help = atoi(lh) != 0;
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     if (getenv("BCHK_NO_TABLE")) c->use_table = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);

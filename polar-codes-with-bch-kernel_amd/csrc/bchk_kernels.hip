@@ -626,6 +626,60 @@ __device__ __forceinline__ void prep_tab_store(PrepTab<M, TMAX> *pt, const Prep<
     }
 }
 
+// ---- cross-workgroup help for long codewords (m >= 7, round 5). A codeword with many chunks
+// left is published as workgroup b's job: its prep tables, and its loop state mirrored from
+// the acceptor (bound, l0, skip key, chunks consumed, done). Workgroups left without a heavy
+// codeword attach to a job, claim chunks from the job's counter (which the owner's decoders
+// claim from too), decode them exactly as the owner's decoders would (long_decode, into their
+// own LDS ring) and hand each chunk's slot record over through the job's data: `sc1` stores,
+// `s_waitcnt vmcnt(0)`, then the chunk's tag (`sc1`). The owner's acceptor polls the tags of
+// the chunks its own ring does not hold yet (only while helpers are attached), copies a
+// tagged record into its ring slot and marks it ready, so the acceptance is unchanged. A
+// dense re-decode is always served by the owner's decoders. The owner re-uses its job only
+// after every helper has left (they leave at `done`).
+constexpr uint32_t kShareMinChunks = 64;  // published / helped while at least this many chunks are left
+constexpr uint32_t kHelpersMax = 16;       // helpers per job (the ring window bounds the useful number)
+struct alignas(128) JobCtl {
+    uint32_t state;     // 1: published (prep tables valid), 0: not
+    uint32_t helpers;   // helper workgroups attached
+    uint32_t done;      // the codeword's search has ended
+    uint32_t consumed;  // chunks the acceptor has finished
+    uint32_t next;      // chunk claim counter (owner's decoders and helpers)
+    uint32_t helped;    // some helper has attached to this codeword (sticky until the next)
+    uint64_t bound;     // published loop bound
+    uint64_t l0bits;    // published l0 (f64 bits)
+    uint64_t skey;      // published skip key
+    uint32_t pad[20];
+};
+static_assert(sizeof(JobCtl) == 128, "one control line per job");
+template <int M, int TMAX>
+struct JobData {
+    uint64_t tag[kLongSlots];                 // chunk + 1 once rec[chunk % kLongSlots] is stored
+    LongSlot<Geo<M>::NW> rec[kLongSlots];
+    PrepTab<M, TMAX> pt;
+    uint64_t ordl[32];                        // the order's first 256 positions (bytes)
+    double ap[256];                           // |alpha| by position
+};
+__device__ __forceinline__ uint32_t g_ld32(const uint32_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_st32(uint32_t *a, uint32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t g_ld64(const uint64_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_st64(uint64_t *a, uint64_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// n 8-B words, one wave: LDS -> job data (sc1) or job data -> LDS (sc1 loads)
+__device__ __forceinline__ void job_put(uint64_t *dst, const uint64_t *src, int n, int lane) {
+    for (int i = lane; i < n; i += 64) g_st64(dst + i, src[i]);
+}
+__device__ __forceinline__ void job_get(uint64_t *dst, const uint64_t *src, int n, int first, int stride) {
+    for (int i = first; i < n; i += stride) dst[i] = g_ld64(src + i);
+}
+
 // A decoder wave's work (m >= 7), one call site for both kinds:
 //  * a claim of nch <= kLongClaim chunks c .. c + nch - 1: the patterns skip_lane leaves,
 //    packed 64 per round (the k-th of them in lane k), decoded; each success goes, in pattern
@@ -808,13 +862,19 @@ kaneko_coop_kernel(SearchParams p) {
     double *ap = as + NP;
     uint8_t *ordl = wbase + NP * 16;
     const uint64_t capc = p.max_decodes ? ((p.max_decodes + 63) & ~63ull) : ~0ull;
+    // m >= 7: this workgroup's job (cross-workgroup help), null when off
+    JobCtl *const jcb = (NW > 1) ? reinterpret_cast<JobCtl *>(p.long_jobctl) : nullptr;
+    JobData<M, TMAX> *const jdb = (NW > 1) ? reinterpret_cast<JobData<M, TMAX> *>(p.long_jobs) : nullptr;
+    JobCtl *const jc = jcb ? jcb + blockIdx.x : nullptr;
+    JobData<M, TMAX> *const jd = jdb ? jdb + blockIdx.x : nullptr;
+    uint32_t hidle = 0;  // helper scans in a row that found no job
     for (;;) {
         // the lane index and t re-read opaquely per codeword: values derived from them are not
         // hoisted out of this persistent loop (they stayed live through the whole body and
         // spilled)
         int lane_o = (int)(threadIdx.x & 63), t_o = p.t;
-        asm volatile("" : "+v"(lane_o), "+s"(t_o));
-        const int lane = lane_o, tt = t_o;
+        asm volatile("" : "+v"(lane_o), "+v"(t_o));
+        const int lane = lane_o, tt = uni(t_o);
 #if BCHK_LONG_GFREP
         const GfRep<M> gfr{grep, 4 * (lane & 15)};
 #else
@@ -823,6 +883,17 @@ kaneko_coop_kernel(SearchParams p) {
         (void)tt;
         __syncthreads();
         if (threadIdx.x == 0) {
+            if (jc) {  // the previous codeword's job: closed, and every helper gone
+                g_st32(&jc->done, 1u);
+                g_st32(&jc->state, 0u);
+                uint32_t sp = 0;
+                while (g_ld32(&jc->helpers) != 0u && ++sp < kSpinLimit) __builtin_amdgcn_s_sleep(8);
+                if (sp >= kSpinLimit) flag_fault(p, kFaultCoopRing);
+                g_st32(&jc->next, 0u);
+                g_st32(&jc->consumed, 0u);
+                g_st32(&jc->helped, 0u);
+                g_st32(&jc->done, 0u);
+            }
             ctl->item = next_heavy(p);
 #ifdef BCHK_DIAG
             ctl->drec = atomicAdd(p.diag_count, 1u);
@@ -837,9 +908,79 @@ kaneko_coop_kernel(SearchParams p) {
         for (uint32_t k = threadIdx.x; k < (uint32_t)kCoopSlots; k += blockDim.x) ctl->ready[k] = 0;
         __syncthreads();
         const uint32_t item = ctl->item;
-        if (item == kEmptySlot) return;
-        if (item >= p.count) continue;  // never a valid slot value: no access outside the batch
-        if (threadIdx.x == 0 && p.coop_stats) atomicAdd(p.coop_stats + 1, 1u);
+        JobCtl *hq = nullptr;  // helper mode (m >= 7): the job this workgroup helps
+        if (item == kEmptySlot) {
+            if constexpr (NW > 1) {
+                if (jc) {
+                    // ---------------------------------------------- helper (m >= 7)
+                    // wave 0 picks the published job with the most chunks left and attaches;
+                    // the workgroup loads its tables and runs the decoder loop below on it
+                    __shared__ uint32_t hjob;
+                    if (threadIdx.x < 64) {
+                        uint64_t key = 0;
+                        for (uint32_t j = (uint32_t)lane; j < gridDim.x; j += 64) {
+                            const JobCtl *q = jcb + j;
+                            if (j == blockIdx.x || g_ld32(&q->state) != 1u || g_ld32(&q->done) ||
+                                g_ld32(&q->helpers) >= kHelpersMax)
+                                continue;
+                            const uint64_t bch = (g_ld64(&q->bound) + 63ull) >> 6, nx = g_ld32(&q->next);
+                            const uint64_t left = bch > nx ? bch - nx : 0ull;
+                            const uint64_t kj = ((left < (1ull << 39) ? left : (1ull << 39) - 1ull) << 24) | j;
+                            if (left >= kShareMinChunks && kj > key) key = kj;
+                        }
+#pragma unroll
+                        for (int o = 32; o; o >>= 1) {
+                            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, o, 64);
+                            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), o, 64);
+                            const uint64_t other = ((uint64_t)hi << 32) | lo;
+                            key = other > key ? other : key;
+                        }
+                        if (lane == 0) {
+                            uint32_t pick = kEmptySlot;
+                            if (key) {
+                                const uint32_t j = (uint32_t)(key & 0xFFFFFFu);
+                                JobCtl *q = jcb + j;
+                                const uint32_t h = atomicAdd(&q->helpers, 1u);
+                                // attached first, then the state: an owner that saw no helper may
+                                // have closed it, or published its next codeword (whose tables
+                                // were stored before its state)
+                                if (h < kHelpersMax && g_ld32(&q->state) == 1u && !g_ld32(&q->done)) {
+                                    pick = j;
+                                    g_st32(&q->helped, 1u);  // the acceptor polls tags from now on
+                                } else {
+                                    atomicSub(&q->helpers, 1u);
+                                }
+                            }
+                            hjob = pick;
+                        }
+                    }
+                    __syncthreads();
+                    const uint32_t jb = (uint32_t)uni((int)hjob);
+                    if (jb == kEmptySlot) {
+                        if (++hidle > 16u) return;
+                        __builtin_amdgcn_s_sleep(127);
+                        continue;
+                    }
+                    hidle = 0;
+                    hq = jcb + jb;
+                    const JobData<M, TMAX> *qd = jdb + jb;
+                    // the job's tables into this workgroup's LDS (sc1 loads, behind the barrier
+                    // that follows wave 0's state poll)
+                    job_get(reinterpret_cast<uint64_t *>(ptab), reinterpret_cast<const uint64_t *>(&qd->pt),
+                            (int)(sizeof(PrepTab<M, TMAX>) / 8), (int)threadIdx.x, (int)blockDim.x);
+                    job_get(reinterpret_cast<uint64_t *>(ordl), qd->ordl, NP / 8, (int)threadIdx.x, (int)blockDim.x);
+                    job_get(reinterpret_cast<uint64_t *>(ap), reinterpret_cast<const uint64_t *>(qd->ap), NP,
+                            (int)threadIdx.x, (int)blockDim.x);
+                    __syncthreads();
+                }
+            }
+            if (!hq) return;
+        } else if (item >= p.count) {
+            continue;  // never a valid slot value: no access outside the batch
+        }
+        const bool helper = hq != nullptr;
+        JobData<M, TMAX> *const hqd = helper ? jdb + (hq - jcb) : nullptr;
+        if (threadIdx.x == 0 && p.coop_stats && !helper) atomicAdd(p.coop_stats + 1, 1u);
         const uint32_t cw = item;
 #ifdef BCHK_DIAG
         const uint32_t drec = ctl->drec;  // this codeword's diagnostic record
@@ -851,8 +992,10 @@ kaneko_coop_kernel(SearchParams p) {
         const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
         Prep<M, TMAX> P;  // every wave builds the same prep (its own LDS slice)
-        prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
         SearchState<NW> S;
+        bool pub = false;  // the acceptor: this codeword was published as a job
+        if (!helper) {
+        prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
         init_state<M>(S, p.variant);
         if (threadIdx.x == 0) {
             ctl->bound = S.bound;
@@ -876,6 +1019,22 @@ kaneko_coop_kernel(SearchParams p) {
             if (wid == kAcceptor) {
                 first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
                 const uint64_t skey0 = S.accepted ? skip_key<M, TMAX>(S.best, P, lane) : 0ull;
+                if (jc && !S.done && ((S.bound + 63ull) >> 6) >= 2ull * kShareMinChunks) {
+                    // publish the job: tags cleared, tables, loop state; then its state
+                    for (int i = lane; i < kLongSlots; i += 64) g_st64(&jd->tag[i], 0ull);
+                    job_put(reinterpret_cast<uint64_t *>(&jd->pt), reinterpret_cast<const uint64_t *>(ptab),
+                            (int)(sizeof(PrepTab<M, TMAX>) / 8), lane);
+                    job_put(jd->ordl, reinterpret_cast<const uint64_t *>(ordl), NP / 8, lane);
+                    job_put(reinterpret_cast<uint64_t *>(jd->ap), reinterpret_cast<const uint64_t *>(ap), NP, lane);
+                    if (lane == 0) {
+                        g_st64(&jc->bound, S.bound);
+                        g_st64(&jc->l0bits, (uint64_t)__double_as_longlong(S.l0));
+                        g_st64(&jc->skey, skey0);
+                    }
+                    mem_drain();
+                    if (lane == 0) g_st32(&jc->state, 1u);
+                    pub = true;
+                }
                 if (lane == 0) {
                     lds_st64(&ctl->bound, S.bound);
                     lds_st64(reinterpret_cast<uint64_t *>(&ctl->l0), (uint64_t)__double_as_longlong(S.l0));
@@ -895,7 +1054,8 @@ kaneko_coop_kernel(SearchParams p) {
                 }
             }
         }
-        if (NW > 1 && wid != kAcceptor) {
+        }  // !helper
+        if (NW > 1 && (helper || wid != kAcceptor)) {
             // ------------------------------------------------ decoder, m >= 7 (packed)
             // One call site of long_decode for both jobs: a dense re-decode the acceptor asks
             // for (served first: it waits on it), else the wave's claim once it fits the ring
@@ -914,28 +1074,43 @@ kaneko_coop_kernel(SearchParams p) {
                         // the last BCHK_LONG_TAIL chunks below the published bound in smaller
                         // claims: the codeword ends with its slowest claim
                         nch = (uint32_t)kLongClaim;
-                        if (BCHK_LONG_TAIL > 0) {
+                        if (BCHK_LONG_TAIL > 0 && !helper) {
                             const uint64_t bch = (lds_ld64(&ctl->bound) + 63ull) >> 6;
-                            if ((uint64_t)lds_ld(&ctl->next) + (uint64_t)BCHK_LONG_TAIL >= bch)
+                            const uint32_t nx = jc ? g_ld32(&jc->next) : lds_ld(&ctl->next);
+                            if ((uint64_t)nx + (uint64_t)BCHK_LONG_TAIL >= bch)
                                 nch = (uint32_t)BCHK_LONG_TAIL_CLAIM;
                         }
-                        c = atomicAdd(&ctl->next, nch);
+                        // (the job's counter when help is on: helpers claim from it too)
+                        JobCtl *const src = helper ? hq : jc;
+                        c = src ? atomicAdd(&src->next, nch) : atomicAdd(&ctl->next, nch);
                     }
-                    c = (uint32_t)__shfl((int)c, 0, 64);
-                    nch = (uint32_t)__shfl((int)nch, 0, 64);
+                    c = (uint32_t)uni(__shfl((int)c, 0, 64));
+                    nch = (uint32_t)uni(__shfl((int)nch, 0, 64));
                     have = true;
                     spins = 0;
                 }
-                if (lds_ld(&ctl->done)) break;
+                // the loop state: this workgroup's LDS, or (helper) the job's mirror, read
+                // wave-uniform (readfirstlane)
+                const bool fin = helper ? uni((int)g_ld32(&hq->done)) != 0 : lds_ld(&ctl->done) != 0u;
+                if (fin || (helper && 64ull * c >= capc)) break;
                 uint32_t r = 0;  // a pending dense request (chunk + 1), taken by one wave
-                if (lane == 0) {
+                if (lane == 0 && !helper) {
                     r = lds_ld(&ctl->redo);
                     if (r && atomicCAS(&ctl->redo, r, 0u) != r) r = 0;
                 }
                 r = (uint32_t)__shfl((int)r, 0, 64);
                 const uint64_t b0 = 64ull * c;
-                const bool ready = c + (uint32_t)(kLongClaim - 1) < lds_ld(&ctl->consumed) + kLongSlots &&
-                                   b0 < lds_ld64(&ctl->bound) && b0 < capc;
+                uint32_t cons;
+                uint64_t bnd;
+                if (helper) {
+                    cons = (uint32_t)uni((int)g_ld32(&hq->consumed));
+                    const uint64_t b = g_ld64(&hq->bound);
+                    bnd = ((uint64_t)(uint32_t)uni((int)(uint32_t)(b >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)b);
+                } else {
+                    cons = lds_ld(&ctl->consumed);
+                    bnd = lds_ld64(&ctl->bound);
+                }
+                const bool ready = c + (uint32_t)(kLongClaim - 1) < cons + kLongSlots && b0 < bnd && b0 < capc;
                 if (!r && !ready) {
                     if (++spins > kSpinLimit) {
 #ifdef BCHK_COOP_DEBUG
@@ -954,13 +1129,30 @@ kaneko_coop_kernel(SearchParams p) {
                 const unsigned long long tw1 = __builtin_amdgcn_s_memtime();
                 dg[5] += tw1 - tw0;  // m >= 7 decoders: cycles waiting (ring space, bound, done)
 #endif
-                const double l0r = __longlong_as_double((long long)lds_ld64(
-                    reinterpret_cast<const uint64_t *>(&ctl->l0)));
-                const uint64_t skey = lds_ld64(&ctl->skey);  // a codeword found before chunk c
+                const double l0r = __longlong_as_double((long long)(helper ? g_ld64(&hq->l0bits) : lds_ld64(
+                    reinterpret_cast<const uint64_t *>(&ctl->l0))));
+                // a codeword found before chunk c
+                const uint64_t skey = helper ? g_ld64(&hq->skey) : lds_ld64(&ctl->skey);
                 const bool dense = r != 0u;
                 const int rounds = long_decode<M, TMAX>(ptab, ordl, dense ? r - 1u : c, capc, l0r, skey, tt, ex, gfr,
                                                         ap, wscr, lring, ldense, ctl, lane, dense ? 1u : nch,
                                                         p.long_rec, dense);
+                if (helper) {
+                    // hand the chunks over: slot records (sc1), drained, then their tags
+                    constexpr int SW = (int)(sizeof(LongSlot<NW>) / 8);
+                    for (uint32_t g = 0; g < nch; ++g) {
+                        const uint32_t cg = c + g;
+                        if (64ull * cg < capc && lane < SW)
+                            g_st64(reinterpret_cast<uint64_t *>(&hqd->rec[cg % kLongSlots]) + lane,
+                                   reinterpret_cast<const uint64_t *>(&lring[cg % kLongSlots])[lane]);
+                    }
+                    mem_drain();
+                    if (lane == 0)
+                        for (uint32_t g = 0; g < nch; ++g) {
+                            const uint32_t cg = c + g;
+                            if (64ull * cg < capc) g_st64(&hqd->tag[cg % kLongSlots], (uint64_t)cg + 1ull);
+                        }
+                }
                 if (dense) {
                     if (lane == 0) {
                         lds_st(&ctl->redo_done, r);
@@ -1069,7 +1261,30 @@ kaneko_coop_kernel(SearchParams p) {
                 // lane j looks at chunk c + j: the run of consecutive finished chunks is
                 // taken in one batch (one LDS round trip for flags, one for the masks)
                 const uint32_t cj = c + (uint32_t)lane;
-                const bool rdy = lane < kCoopSlots && lds_ld(&ctl->ready[cj % kCoopSlots]) == cj + 1u;
+                bool rdy = lane < kCoopSlots && lds_ld(&ctl->ready[cj % kCoopSlots]) == cj + 1u;
+                if constexpr (NW > 1) {
+                    // chunks a helper decoded (only while helpers are attached): its record
+                    // into our ring slot, then the slot is ready like our decoders' ones
+                    // (sticky: a helper that delivered and left still has tags to be read)
+                    if (pub && uni((int)g_ld32(&jc->helped)) != 0) {
+                        const bool hit =
+                            lane < 16 && !rdy && g_ld64(&jd->tag[cj % kLongSlots]) == (uint64_t)cj + 1ull;
+                        // one record at a time, lane w copying word w (few registers: this wave
+                        // holds the search state)
+                        constexpr int SW = (int)(sizeof(LongSlot<NW>) / 8);
+                        for (uint64_t hm = ballot(hit); hm; hm &= hm - 1) {
+                            const uint32_t cc = c + (uint32_t)__builtin_ctzll(hm);
+                            if (lane < SW)
+                                reinterpret_cast<uint64_t *>(&lring[cc % kLongSlots])[lane] =
+                                    g_ld64(reinterpret_cast<const uint64_t *>(&jd->rec[cc % kLongSlots]) + lane);
+                        }
+                        wave_sync();
+                        if (hit) {
+                            lds_st(&ctl->ready[cj % kCoopSlots], cj + 1u);
+                            rdy = true;
+                        }
+                    }
+                }
                 const uint64_t rm = ballot(rdy);
                 // chunks c .. c + run - 1 ready (all 64 polled: the long-code ring has 128
                 // slots, and ctz of 0 is undefined -- -1 on gfx950)
@@ -1190,6 +1405,12 @@ kaneko_coop_kernel(SearchParams p) {
                              (uint64_t)__double_as_longlong(S.l0));
                     if (M >= 7) lds_st64(&ctl->skey, skey);
                     lds_st(&ctl->consumed, c);
+                    if (pub) {  // the job's mirror for its helpers
+                        g_st64(&jc->bound, S.bound);
+                        g_st64(&jc->l0bits, (uint64_t)__double_as_longlong(S.l0));
+                        g_st64(&jc->skey, skey);
+                        g_st32(&jc->consumed, c);
+                    }
                 }
 #ifdef BCHK_DIAG
                 dg[2] += __builtin_amdgcn_s_memtime() - t_a;
@@ -1198,8 +1419,18 @@ kaneko_coop_kernel(SearchParams p) {
 #endif
             }
             __builtin_amdgcn_s_setprio(0);
-            if (lane == 0) lds_st(&ctl->done, 1u);
+            if (lane == 0) {
+                lds_st(&ctl->done, 1u);
+                if (jc) g_st32(&jc->done, 1u);  // helpers leave
+            }
             write_outputs<M, TMAX>(S, P, p, cw, lane);
+        }
+        if constexpr (NW > 1) {
+            if (helper) {  // every wave has left the job: detach, then look for another
+                __syncthreads();
+                if (threadIdx.x == 0) atomicSub(&hq->helpers, 1u);
+                continue;
+            }
         }
 #ifdef BCHK_DIAG
         // chunk counts of every wave into the acceptor's record
@@ -1437,6 +1668,7 @@ static KernelSet make_set() {
         k.tail_block_bytes = (size_t)help_bytes<M, TMAX>();
     }
     k.coop_threads = kWaveSize * coop_waves<M>();
+    k.long_job_bytes = Geo<M>::NW > 1 ? sizeof(JobData<M, TMAX>) : 0;
     k.coop_bytes = coop;
     k.alg = &launch_alg_impl<M, TMAX>;
     k.tmax = TMAX;

@@ -775,3 +775,29 @@ def test_lane_prepass_equals_first_kernel(m, t, J, snr):
         np.testing.assert_array_equal(a[1][idx][acc].view(np.uint64), l2[acc].view(np.uint64))
     finally:
         off.close()
+
+
+@pytest.mark.parametrize("snr,J,cap", [(6.0, -1, 0), (5.0, 15, 0), (6.0, -1, 1 << 16)])
+def test_long_help_equals_no_help(snr, J, cap):
+    # m >= 7: cooperative workgroups left without a heavy codeword help the published ones
+    # (chunks decoded by other workgroups, handed over through the job's tags and records).
+    # Words, l0 bits and every stats field equal a context without help, with and without a
+    # decode cap (helpers stop at the cap; the acceptor still reads what they delivered)
+    m, t = 8, 15
+    on = dec(m, t, J=J)
+    off = _ctx_env(m, t, J, BCHK_LONG_HELP=0)
+    try:
+        _, y, _ = on.generate(snr, 1 << (17 if J < 0 else 15), seed=83)
+        outs = []
+        for d in (on, off):
+            d.set_max_decodes(cap)
+            outs.append(d.decode(y))
+            d.set_max_decodes(0)
+        a, b = outs
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
+        np.testing.assert_array_equal(a[2], b[2])
+        # codewords long enough to be published (>= 128 chunks) exist
+        assert (a[2]["decodes"] > 64 * 128).sum() >= 1, np.sort(a[2]["decodes"])[-8:]
+    finally:
+        off.close()
