@@ -159,8 +159,10 @@ struct SearchParams {
     // is job b: its control line (jobctl, 128 B each, zeroed per launch) and its data
     // (jobs, KernelSet::long_job_bytes each: result tags and records, the prep tables).
     // Workgroups left without a heavy codeword decode chunks of the published ones.
-    void *long_jobctl;
+    void *long_jobctl;     // [gridDim + 1] lines: the last one counts the workgroups owning a codeword
     void *long_jobs;
+    uint32_t long_help_max;   // helpers per job (0: kHelpersMax)
+    uint32_t long_share_min;  // chunks left for a job to be offered (0: kShareMinChunks)
 };
 constexpr int kCntSlots = 512;
 constexpr int kCntStride = 16;  // u64 per slot: one 128-B line

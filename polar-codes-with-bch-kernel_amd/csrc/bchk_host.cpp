@@ -442,6 +442,7 @@ struct bchk_ctx {
     bool lane_pre = true;
     // m >= 7: idle cooperative workgroups help the running long codewords (BCHK_LONG_HELP=0: off)
     bool long_help = true;
+    uint32_t long_help_max = 0, long_share_min = 0;  // BCHK_LONG_HELP_MAX / BCHK_LONG_SHARE_MIN (0: defaults)
     DevBuf syn8;  // its hard-decision syndrome table (SearchParams::syn8)
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
@@ -776,12 +777,14 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
     }
     if (p.heavy_tail) {
         if (c->m >= 7 && c->long_help && c->ks.long_job_bytes) {  // jobs of the cooperative workgroups
-            if ((rc = P.jobctl.ensure((size_t)grid_coop * 128)) ||
+            if ((rc = P.jobctl.ensure((size_t)(grid_coop + 1) * 128)) ||
                 (rc = P.jobs.ensure((size_t)grid_coop * c->ks.long_job_bytes)))
                 return rc;
-            HIP_TRY(hipMemsetAsync(P.jobctl.p, 0, (size_t)grid_coop * 128, cs));
+            HIP_TRY(hipMemsetAsync(P.jobctl.p, 0, (size_t)(grid_coop + 1) * 128, cs));
             pc.long_jobctl = P.jobctl.p;
             pc.long_jobs = P.jobs.p;
+            pc.long_help_max = c->long_help_max;
+            pc.long_share_min = c->long_share_min;
         }
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));
         HIP_TRY(launch_coop(c->ks, pc, grid_coop, c->lds_coop, cs));
@@ -919,6 +922,8 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     }
     if (const char *lp = getenv("BCHK_LANE_PRE")) c->lane_pre = atoi(lp) != 0;
     if (const char *lh = getenv("BCHK_LONG_HELP")) c->long_help = atoi(lh) != 0;
+    if (const char *hm = getenv("BCHK_LONG_HELP_MAX")) c->long_help_max = (uint32_t)std::max(1, atoi(hm));
+    if (const char *sm = getenv("BCHK_LONG_SHARE_MIN")) c->long_share_min = (uint32_t)std::max(8, atoi(sm));
     if (getenv("BCHK_NO_FAST")) c->use_fast = false;
     if (getenv("BCHK_NO_TABLE")) c->use_table = false;
     if (const char *cl = getenv("BCHK_CHUNK_LIMIT")) c->chunk_limit = (uint32_t)atoi(cl);

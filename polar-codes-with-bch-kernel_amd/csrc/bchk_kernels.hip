@@ -868,6 +868,11 @@ kaneko_coop_kernel(SearchParams p) {
     JobCtl *const jc = jcb ? jcb + blockIdx.x : nullptr;
     JobData<M, TMAX> *const jd = jdb ? jdb + blockIdx.x : nullptr;
     uint32_t hidle = 0;  // helper scans in a row that found no job
+    // the workgroups owning a codeword (helpers keep looking while any does)
+    uint32_t *const owners = jcb ? reinterpret_cast<uint32_t *>(jcb + gridDim.x) : nullptr;
+    const uint32_t help_max = p.long_help_max ? p.long_help_max : kHelpersMax;
+    const uint32_t share_min = p.long_share_min ? p.long_share_min : kShareMinChunks;
+    bool owning = false;  // thread 0: this workgroup counts among the owners
     for (;;) {
         // the lane index and t re-read opaquely per codeword: values derived from them are not
         // hoisted out of this persistent loop (they stayed live through the whole body and
@@ -894,7 +899,15 @@ kaneko_coop_kernel(SearchParams p) {
                 g_st32(&jc->helped, 0u);
                 g_st32(&jc->done, 0u);
             }
+            if (owning) {
+                atomicSub(owners, 1u);
+                owning = false;
+            }
             ctl->item = next_heavy(p);
+            if (owners && ctl->item != kEmptySlot && ctl->item < p.count) {
+                atomicAdd(owners, 1u);
+                owning = true;
+            }
 #ifdef BCHK_DIAG
             ctl->drec = atomicAdd(p.diag_count, 1u);
 #endif
@@ -944,7 +957,7 @@ kaneko_coop_kernel(SearchParams p) {
                                 // attached first, then the state: an owner that saw no helper may
                                 // have closed it, or published its next codeword (whose tables
                                 // were stored before its state)
-                                if (h < kHelpersMax && g_ld32(&q->state) == 1u && !g_ld32(&q->done)) {
+                                if (h < help_max && g_ld32(&q->state) == 1u && !g_ld32(&q->done)) {
                                     pick = j;
                                     g_st32(&q->helped, 1u);  // the acceptor polls tags from now on
                                 } else {
@@ -957,7 +970,9 @@ kaneko_coop_kernel(SearchParams p) {
                     __syncthreads();
                     const uint32_t jb = (uint32_t)uni((int)hjob);
                     if (jb == kEmptySlot) {
-                        if (++hidle > 16u) return;
+                        // no job now: wait while some workgroup still owns a codeword (it may
+                        // publish one), leave when none does (bounded: a logic error ends it)
+                        if (uni((int)g_ld32(owners)) == 0 || ++hidle > (1u << 16)) return;
                         __builtin_amdgcn_s_sleep(127);
                         continue;
                     }
@@ -1019,7 +1034,7 @@ kaneko_coop_kernel(SearchParams p) {
             if (wid == kAcceptor) {
                 first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
                 const uint64_t skey0 = S.accepted ? skip_key<M, TMAX>(S.best, P, lane) : 0ull;
-                if (jc && !S.done && ((S.bound + 63ull) >> 6) >= 2ull * kShareMinChunks) {
+                if (jc && !S.done && ((S.bound + 63ull) >> 6) >= 2ull * share_min) {
                     // publish the job: tags cleared, tables, loop state; then its state
                     for (int i = lane; i < kLongSlots; i += 64) g_st64(&jd->tag[i], 0ull);
                     job_put(reinterpret_cast<uint64_t *>(&jd->pt), reinterpret_cast<const uint64_t *>(ptab),
@@ -1267,16 +1282,30 @@ kaneko_coop_kernel(SearchParams p) {
                     // into our ring slot, then the slot is ready like our decoders' ones
                     // (sticky: a helper that delivered and left still has tags to be read)
                     if (pub && uni((int)g_ld32(&jc->helped)) != 0) {
+                        constexpr int HC = 32;  // chunks c .. c + HC - 1 looked up
                         const bool hit =
-                            lane < 16 && !rdy && g_ld64(&jd->tag[cj % kLongSlots]) == (uint64_t)cj + 1ull;
-                        // one record at a time, lane w copying word w (few registers: this wave
-                        // holds the search state)
+                            lane < HC && !rdy && g_ld64(&jd->tag[cj % kLongSlots]) == (uint64_t)cj + 1ull;
+                        // the tagged records, all words in flight at once: word w of chunk j at
+                        // index j SW + w, lane = index mod 64
                         constexpr int SW = (int)(sizeof(LongSlot<NW>) / 8);
-                        for (uint64_t hm = ballot(hit); hm; hm &= hm - 1) {
-                            const uint32_t cc = c + (uint32_t)__builtin_ctzll(hm);
-                            if (lane < SW)
-                                reinterpret_cast<uint64_t *>(&lring[cc % kLongSlots])[lane] =
-                                    g_ld64(reinterpret_cast<const uint64_t *>(&jd->rec[cc % kLongSlots]) + lane);
+                        const uint64_t hm = ballot(hit);
+                        if (hm) {
+                            uint64_t v[(HC * SW + 63) / 64];
+#pragma unroll
+                            for (int k = 0; k < (HC * SW + 63) / 64; ++k) {
+                                const int idx = lane + 64 * k, j = idx / SW, w = idx - SW * (idx / SW);
+                                const uint32_t cc = c + (uint32_t)j;
+                                v[k] = (idx < HC * SW && ((hm >> j) & 1ull))
+                                           ? g_ld64(reinterpret_cast<const uint64_t *>(&jd->rec[cc % kLongSlots]) + w)
+                                           : 0ull;
+                            }
+#pragma unroll
+                            for (int k = 0; k < (HC * SW + 63) / 64; ++k) {
+                                const int idx = lane + 64 * k, j = idx / SW, w = idx - SW * (idx / SW);
+                                const uint32_t cc = c + (uint32_t)j;
+                                if (idx < HC * SW && ((hm >> j) & 1ull))
+                                    reinterpret_cast<uint64_t *>(&lring[cc % kLongSlots])[w] = v[k];
+                            }
                         }
                         wave_sync();
                         if (hit) {
