@@ -406,9 +406,11 @@ kaneko_first_kernel(SearchParams p) {
 // Long-code ring slots and tail claims (experiment builds vary them; BCH(255,139,31), 2^20,
 // cooperative kernel at 5 dB J=15 / 6 dB J=inf: 128 slots 85.1 / 11.0 ms, 256 slots 82.9 /
 // 9.9, + 4-chunk claims in the last 60 chunks 81.1-81.6 / 9.8-9.9, 384 slots 81.1 / 9.7;
-// profiles/r04_long/coop_ring*.jsonl)
+// profiles/r04_long/coop_ring*.jsonl). Round 5, with helper workgroups (the ring is also the
+// window of chunks helpers may run ahead): 256 slots 64.2 / 1.57 ms, 512 64.2 / 1.17, 1024
+// 64.3 / 1.07 (profiles/r05_long/help_ring_slots.jsonl)
 #ifndef BCHK_LONG_SLOTS
-#define BCHK_LONG_SLOTS 256
+#define BCHK_LONG_SLOTS 1024
 #endif
 #ifndef BCHK_LONG_TAIL
 #define BCHK_LONG_TAIL 60
