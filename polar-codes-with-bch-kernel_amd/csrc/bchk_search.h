@@ -787,8 +787,14 @@ __device__ __forceinline__ void first_patterns(SearchState<Geo<M>::NW> &S, const
 // (chunks, as before), and from i* on every improvement has l < l0 <= lim, so it is among
 // the enumerated candidates. Nothing fits (stack, candidate list, kernel dimension,
 // budget): the codeword is handed to the cooperative kernel as before.
-constexpr int kAnStack = 448;            // pending nodes of the enumeration (64 lanes x depth)
-constexpr int kAnCand = 128;             // candidate codewords kept for the replay
+#ifndef BCHK_AN_STACK
+#define BCHK_AN_STACK 448
+#endif
+#ifndef BCHK_AN_CAND
+#define BCHK_AN_CAND 128
+#endif
+constexpr int kAnStack = BCHK_AN_STACK;  // pending nodes of the enumeration (64 lanes x depth)
+constexpr int kAnCand = BCHK_AN_CAND;    // candidate codewords kept for the replay
 constexpr int kAnKern = 3;               // kernel dimension of R's columns (2^3 combinations)
 constexpr uint32_t kAnBudget = 4096;     // enumeration nodes per attempt
 constexpr uint32_t kAnExactChunks = 32;  // exact chunks below the split pattern
