@@ -161,6 +161,7 @@ struct SearchParams {
     // Workgroups left without a heavy codeword decode chunks of the published ones.
     void *long_jobctl;     // [gridDim + 1] lines: the last one counts the workgroups owning a codeword
     void *long_jobs;
+    uint32_t long_epoch;      // launch count (the high bits of the jobs' tag generations)
     uint32_t long_help_max;   // helpers per job (0: kHelpersMax)
     uint32_t long_share_min;  // chunks left for a job to be offered (0: kShareMinChunks)
 };

@@ -442,7 +442,8 @@ struct bchk_ctx {
     bool lane_pre = true;
     // m >= 7: idle cooperative workgroups help the running long codewords (BCHK_LONG_HELP=0: off)
     bool long_help = true;
-    uint32_t long_help_max = 0, long_share_min = 0;  // BCHK_LONG_HELP_MAX / BCHK_LONG_SHARE_MIN (0: defaults)
+    uint32_t long_help_max = 0, long_share_min = 0;
+    uint32_t long_epoch = 0;  // cooperative launches with jobs (tag generations)  // BCHK_LONG_HELP_MAX / BCHK_LONG_SHARE_MIN (0: defaults)
     DevBuf syn8;  // its hard-decision syndrome table (SearchParams::syn8)
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
@@ -784,6 +785,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             pc.long_jobctl = P.jobctl.p;
             pc.long_jobs = P.jobs.p;
             pc.long_help_max = c->long_help_max;
+            pc.long_epoch = ++c->long_epoch;
             pc.long_share_min = c->long_share_min;
         }
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));

@@ -651,12 +651,13 @@ struct alignas(128) JobCtl {
     uint64_t bound;     // published loop bound
     uint64_t l0bits;    // published l0 (f64 bits)
     uint64_t skey;      // published skip key
-    uint32_t pad[20];
+    uint32_t gen;       // this publication's generation: the high word of its tags
+    uint32_t pad[19];
 };
 static_assert(sizeof(JobCtl) == 128, "one control line per job");
 template <int M, int TMAX>
 struct JobData {
-    uint64_t tag[kLongSlots];                 // chunk + 1 once rec[chunk % kLongSlots] is stored
+    uint64_t tag[kLongSlots];                 // gen << 32 | chunk + 1 once rec[chunk % kLongSlots] is stored
     LongSlot<Geo<M>::NW> rec[kLongSlots];
     PrepTab<M, TMAX> pt;
     uint64_t ordl[32];                        // the order's first 256 positions (bytes)
@@ -875,6 +876,11 @@ kaneko_coop_kernel(SearchParams p) {
     const uint32_t help_max = p.long_help_max ? p.long_help_max : kHelpersMax;
     const uint32_t share_min = p.long_share_min ? p.long_share_min : kShareMinChunks;
     bool owning = false;  // thread 0: this workgroup counts among the owners
+    uint32_t *const idle_wgs = owners ? owners + 1 : nullptr;  // workgroups that have turned helper
+    bool was_helper = false;  // thread 0: counted in idle_wgs
+    // publication generations: the launch's epoch above a per-workgroup count (a tag of an
+    // earlier publication, or of an earlier launch, never matches)
+    uint32_t jgen = (p.long_epoch & 0xFFFFFu) << 12;
     for (;;) {
         // the lane index and t re-read opaquely per codeword: values derived from them are not
         // hoisted out of this persistent loop (they stayed live through the whole body and
@@ -969,6 +975,10 @@ kaneko_coop_kernel(SearchParams p) {
                             hjob = pick;
                         }
                     }
+                    if (threadIdx.x == 0 && !was_helper) {
+                        atomicAdd(idle_wgs, 1u);  // owners publish their long codewords from now on
+                        was_helper = true;
+                    }
                     __syncthreads();
                     const uint32_t jb = (uint32_t)uni((int)hjob);
                     if (jb == kEmptySlot) {
@@ -1011,6 +1021,25 @@ kaneko_coop_kernel(SearchParams p) {
         Prep<M, TMAX> P;  // every wave builds the same prep (its own LDS slice)
         SearchState<NW> S;
         bool pub = false;  // the acceptor: this codeword was published as a job
+        // the acceptor wave publishes its codeword as a job: tables, loop state, generation
+        // (drained), then the state word
+        auto publish = [&](uint64_t sk, uint32_t cons) {
+            jgen = (jgen & ~0xFFFu) | ((jgen + 1u) & 0xFFFu);
+            job_put(reinterpret_cast<uint64_t *>(&jd->pt), reinterpret_cast<const uint64_t *>(ptab),
+                    (int)(sizeof(PrepTab<M, TMAX>) / 8), lane);
+            job_put(jd->ordl, reinterpret_cast<const uint64_t *>(ordl), NP / 8, lane);
+            job_put(reinterpret_cast<uint64_t *>(jd->ap), reinterpret_cast<const uint64_t *>(ap), NP, lane);
+            if (lane == 0) {
+                g_st32(&jc->gen, jgen);
+                g_st64(&jc->bound, S.bound);
+                g_st64(&jc->l0bits, (uint64_t)__double_as_longlong(S.l0));
+                g_st64(&jc->skey, sk);
+                g_st32(&jc->consumed, cons);
+            }
+            mem_drain();
+            if (lane == 0) g_st32(&jc->state, 1u);
+            pub = true;
+        };
         if (!helper) {
         prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
         init_state<M>(S, p.variant);
@@ -1036,22 +1065,8 @@ kaneko_coop_kernel(SearchParams p) {
             if (wid == kAcceptor) {
                 first_patterns<M, TMAX>(S, P, p, ex, lg, as, ap, lane);
                 const uint64_t skey0 = S.accepted ? skip_key<M, TMAX>(S.best, P, lane) : 0ull;
-                if (jc && !S.done && ((S.bound + 63ull) >> 6) >= 2ull * share_min) {
-                    // publish the job: tags cleared, tables, loop state; then its state
-                    for (int i = lane; i < kLongSlots; i += 64) g_st64(&jd->tag[i], 0ull);
-                    job_put(reinterpret_cast<uint64_t *>(&jd->pt), reinterpret_cast<const uint64_t *>(ptab),
-                            (int)(sizeof(PrepTab<M, TMAX>) / 8), lane);
-                    job_put(jd->ordl, reinterpret_cast<const uint64_t *>(ordl), NP / 8, lane);
-                    job_put(reinterpret_cast<uint64_t *>(jd->ap), reinterpret_cast<const uint64_t *>(ap), NP, lane);
-                    if (lane == 0) {
-                        g_st64(&jc->bound, S.bound);
-                        g_st64(&jc->l0bits, (uint64_t)__double_as_longlong(S.l0));
-                        g_st64(&jc->skey, skey0);
-                    }
-                    mem_drain();
-                    if (lane == 0) g_st32(&jc->state, 1u);
-                    pub = true;
-                }
+                if (jc && !S.done && ((S.bound + 63ull) >> 6) >= share_min && uni((int)g_ld32(idle_wgs)) != 0)
+                    publish(skey0, 0u);
                 if (lane == 0) {
                     lds_st64(&ctl->bound, S.bound);
                     lds_st64(reinterpret_cast<uint64_t *>(&ctl->l0), (uint64_t)__double_as_longlong(S.l0));
@@ -1164,11 +1179,13 @@ kaneko_coop_kernel(SearchParams p) {
                                    reinterpret_cast<const uint64_t *>(&lring[cg % kLongSlots])[lane]);
                     }
                     mem_drain();
-                    if (lane == 0)
+                    if (lane == 0) {
+                        const uint64_t tg = (uint64_t)g_ld32(&hq->gen) << 32;  // fixed while attached
                         for (uint32_t g = 0; g < nch; ++g) {
                             const uint32_t cg = c + g;
-                            if (64ull * cg < capc) g_st64(&hqd->tag[cg % kLongSlots], (uint64_t)cg + 1ull);
+                            if (64ull * cg < capc) g_st64(&hqd->tag[cg % kLongSlots], tg | ((uint64_t)cg + 1ull));
                         }
+                    }
                 }
                 if (dense) {
                     if (lane == 0) {
@@ -1286,7 +1303,8 @@ kaneko_coop_kernel(SearchParams p) {
                     if (pub && uni((int)g_ld32(&jc->helped)) != 0) {
                         constexpr int HC = 32;  // chunks c .. c + HC - 1 looked up
                         const bool hit =
-                            lane < HC && !rdy && g_ld64(&jd->tag[cj % kLongSlots]) == (uint64_t)cj + 1ull;
+                            lane < HC && !rdy &&
+                            g_ld64(&jd->tag[cj % kLongSlots]) == (((uint64_t)jgen << 32) | ((uint64_t)cj + 1ull));
                         // the tagged records, all words in flight at once: word w of chunk j at
                         // index j SW + w, lane = index mod 64
                         constexpr int SW = (int)(sizeof(LongSlot<NW>) / 8);
@@ -1443,6 +1461,11 @@ kaneko_coop_kernel(SearchParams p) {
                         g_st32(&jc->consumed, c);
                     }
                 }
+                // published once some workgroup has run out of codewords and enough chunks
+                // are left (a codeword started earlier is published mid-way)
+                if (jc && !pub && !S.done && ((S.bound + 63ull) >> 6) >= (uint64_t)c + share_min &&
+                    uni((int)g_ld32(idle_wgs)) != 0)
+                    publish(skey, c);
 #ifdef BCHK_DIAG
                 dg[2] += __builtin_amdgcn_s_memtime() - t_a;
                 dg[4] += (uint64_t)run;
