@@ -193,7 +193,7 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
                                                const uint64_t *chien, const uint32_t *k, uint32_t kmax_real,
                                                bool bad, uint64_t yH, Rd0 rd0, Rd1 rd1, Between between,
                                                bool live, int t, double s2, const uint32_t *lo = nullptr,
-                                               bool have_lo = false) {
+                                               bool have_lo = false, const uint32_t *syn8 = nullptr) {
     constexpr int N = Geo<M>::N;
     constexpr int W = (TMAX + 3) / 4;
     // calcRightSide takes the first border = 2t+1-m agreeing sorted positions; with m0 == m
@@ -228,15 +228,27 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
     for (int r = 0; r < NPF; ++r) pre[r] = k[r];
     const int o0 = (int)(k[0] & 63u);
     const double c2 = 2.0 / s2;
-    // ---- syndrome of the hard decision (Decoder::findSyndromPoly :184-207)
+    // ---- syndrome of the hard decision (Decoder::findSyndromPoly :184-207): from the byte
+    // table when given (syn8[j][v]: byte value v at positions 8j .. 8j + 7; one L1-resident
+    // load per byte of yH instead of a select and W XORs per position), else per position
     uint32_t S0[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) S0[w] = 0;
+    if (syn8) {
 #pragma unroll
-    for (int pos = 0; pos < N; ++pos) {
-        const uint32_t on = ((yH >> pos) & 1ull) ? 0xFFFFFFFFu : 0u;
+        for (int j = 0; 8 * j < N; ++j) {
+            const uint32_t v = (uint32_t)(yH >> (8 * j)) & 255u;
+            const uint32_t *e = syn8 + ((uint32_t)j * 256u + v) * (uint32_t)W;
 #pragma unroll
-        for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w] & on;
+            for (int w = 0; w < W; ++w) S0[w] ^= e[w];
+        }
+    } else {
+#pragma unroll
+        for (int pos = 0; pos < N; ++pos) {
+            const uint32_t on = ((yH >> pos) & 1ull) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+            for (int w = 0; w < W; ++w) S0[w] ^= col[pos * W + w] & on;
+        }
     }
     // calcL (:69-77, index order) and calcRightSide (:54-67, sorted order) for `diff`
     // (at most t + 1 positions: the error pattern, plus the flipped bit at i = 1).
@@ -785,7 +797,7 @@ kaneko_fast_ring_kernel(SearchParams p) {
         const FastRes R = fast_decide<M, TMAX>(
             ex, lg, col, chien, kept, kmax_real, false, yH, [&](int pos) { return hold ? lrow[pos] : yrow[pos]; },
             [&](int pos) { return yrow[pos]; }, [&] { if (hold) release(); }, live, t, s2,
-            lo, use_lo);
+            lo, use_lo, p.syn8);
 
         // ---- outputs
         const bool resolved = live && R.state != 0;

@@ -666,6 +666,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
         if (c->m <= 6) {
             f.fast_waves = c->fast_waves;
             f.fast_mode = c->fast_mode;
+            f.syn8 = (const uint32_t *)c->syn8.p;  // null unless built
         }
         if (lane) {
             f.pre_mask = (uint64_t *)P.pre.p;
@@ -906,8 +907,9 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (select_fast(m, t, &c->fast))  // m >= 7: kaneko_first_kernel, the search kernel's layout
         c->lds_fast = m >= 7 ? c->lds : tb + fast_block_waves() * fast_wave_bytes();
     if (m >= 7 && !select_lane(m, t, &c->lane)) c->lane = nullptr;
-    if (c->lane) {
-        // the pre-pass's byte syndrome table from the column table (same word stride W)
+    if (c->lane || (m <= 6 && c->fast)) {
+        // the byte syndrome table of the lane kernels (m >= 7 pre-pass, n <= 63 ring kernel)
+        // from the column table (same word stride W)
         const int n = c->field.n, W = (int)c->td.W, NB = (n + 7) / 8;
         const uint32_t *colh = reinterpret_cast<const uint32_t *>(c->tables_host.data() + c->td.off_col);
         std::vector<uint32_t> syn((size_t)NB * 256 * W, 0u);
