@@ -46,7 +46,10 @@ constexpr int kPolarMaxTrellisKernel = 32;  // the trellis is built for kernels 
 // LDS scratch of kMlStack 12-byte search nodes, the reduced basis and the suffix unions of its
 // non-pivot parts (64 + 65 u64), flip costs and |y| (64 floats each). Phases whose coset has
 // at most 2^kMlEnumBits words are enumerated.
-constexpr int kMlStack = 1536;
+#ifndef BCHK_ML_STACK
+#define BCHK_ML_STACK 768  // (64,32) L=8 2 dB, 8 192 words: 1536 nodes 950, 768 1 159, 512 1 116 codewords/s (profiles/r05_f4/ml_stack_variants.jsonl)
+#endif
+constexpr int kMlStack = BCHK_ML_STACK;
 constexpr int kMlEnumBits = 10;
 constexpr uint32_t kMlScratchBytes = 12u * kMlStack + 8u * 64u + 8u * 65u + 8u + 4u * 64u + 4u * 64u;
 // Matrix layers of size >= the trellis threshold (default 16, BCHK_POLAR_TRELLIS) take their
