@@ -140,20 +140,19 @@ __device__ __forceinline__ uint64_t wave_xor64(uint64_t v) {
 }
 // the metric of the word whose disagreement mask is dis: |y| summed in index order (adding
 // +0 where a position agrees leaves the sum unchanged, so this is the trellis's path sum)
+// Only the set positions are visited, in ascending order: the +0 terms of the index-order
+// sum leave a float sum of non-negative terms unchanged, so the bits are the same, and a lane
+// runs popc(dis) steps instead of l.
+__device__ __forceinline__ uint64_t ml_below(int l) { return l >= 64 ? ~0ull : ((1ull << l) - 1ull); }
 __device__ __forceinline__ float ml_metric(uint64_t dis, const float *ay, int l) {
     float m = 0.0f;
-    for (int j = 0; j < l; ++j) m += ((dis >> j) & 1ull) ? ay[j] : 0.0f;
+    for (uint64_t v = dis & ml_below(l); v; v &= v - 1) m += ay[__builtin_ctzll(v)];
     return m;
 }
-// the same, and (fx) the sum over the subset fix of dis, in one pass
+// the same, and (fx) the sum over the subset fix of dis
 __device__ __forceinline__ void ml_metric2(uint64_t dis, uint64_t fix, const float *ay, int l, float &m, float &fx) {
-    m = 0.0f;
-    fx = 0.0f;
-    for (int j = 0; j < l; ++j) {
-        const float a = ay[j];
-        m += ((dis >> j) & 1ull) ? a : 0.0f;
-        fx += ((fix >> j) & 1ull) ? a : 0.0f;
-    }
+    m = ml_metric(dis, ay, l);
+    fx = ml_metric(fix, ay, l);
 }
 
 __device__ float ml_llr(const uint64_t *kr, int l, int loc, const float *src, const uint8_t *off, int d, int s,
