@@ -127,12 +127,41 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
-__device__ __forceinline__ float wave_minf(float v) {
-    for (int m = 1; m < 64; m <<= 1) {
-        const float o = __shfl_xor(v, m, 64);
-        v = o < v ? o : v;
+// v from lane ^ J without the LDS crossbar: DPP quad permutes (J = 1, 2), row rotates (J = 4,
+// 8) and the gfx950 row / half swaps (J = 16, 32)
+template <int J>
+__device__ __forceinline__ uint32_t xlane(uint32_t v, int lane) {
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    } else if constexpr (J == 4) {
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12C, 0xF, 0xF, false);
+        return (lane & 4) ? dn : up;
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+    } else if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else {
+        static_assert(J == 32, "lane distance");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
     }
-    return v;
+}
+// minimum over the wave of non-negative floats or +inf (their bit patterns order as the
+// values do), by DPP / permlane steps
+__device__ __forceinline__ float wave_minf(float v) {
+    const int lane = (int)__lane_id();
+    uint32_t b = __float_as_uint(v), o;
+    o = xlane<1>(b, lane);  b = o < b ? o : b;
+    o = xlane<2>(b, lane);  b = o < b ? o : b;
+    o = xlane<4>(b, lane);  b = o < b ? o : b;
+    o = xlane<8>(b, lane);  b = o < b ? o : b;
+    o = xlane<16>(b, lane); b = o < b ? o : b;
+    o = xlane<32>(b, lane); b = o < b ? o : b;
+    return __uint_as_float(b);
 }
 __device__ __forceinline__ uint64_t wave_xor64(uint64_t v) {
     for (int m = 1; m < 64; m <<= 1) v ^= shfl_xor64(v, m);
