@@ -54,6 +54,11 @@ __device__ constexpr uint8_t kGreen16[60][2] = {
     {3, 5},  {6, 8},  {7, 9},  {10, 12},
     {3, 4},  {5, 6},  {7, 8},  {9, 10}, {11, 12},
     {6, 7},  {8, 9}};
+// accept: leave the flipped-position loops once no lane of the wave has another position
+#ifndef BCHK_ACC_BREAK
+#define BCHK_ACC_BREAK 1
+#endif
+
 template <int O>
 __device__ __forceinline__ void sort16(uint32_t *key) {
 #pragma unroll
@@ -257,10 +262,15 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
         const int m = __popcll(diff);
         const int border = (2 * t + 1) - m;  // m0 == m on both fast-path exits
         double g[LMAX];
+#pragma unroll
+        for (int j = 0; j < LMAX; ++j) g[j] = 0.0;
         uint64_t v = diff;
 #pragma unroll
         for (int j = 0; j < LMAX; ++j) {  // independent loads, issued together; only the
-            g[j] = 0.0;                    // flipped positions' (no line fetched for others)
+                                           // flipped positions' (no line fetched for others)
+#if BCHK_ACC_BREAK
+            if (!ballot(v != 0ull)) break;  // no lane has a j-th flipped position
+#endif
             const int pj = (int)__builtin_ctzll(v);
             bool found = false;
             if (have_lo) {
@@ -283,6 +293,9 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
         v = diff;
 #pragma unroll
         for (int j = 0; j < LMAX; ++j) {
+#if BCHK_ACC_BREAK
+            if (!ballot(v != 0ull)) break;
+#endif
             if (v) l += fabs((2.0 * g[j]) / s2);
             v &= v - 1;
         }
@@ -1180,9 +1193,14 @@ __device__ __forceinline__ LaneRes<Geo<M>::NW> lane_decide(const uint8_t *ex, co
         const int m = mask_popc<NW>(diff);
         const int border = (2 * t + 1) - m;
         double g[LMAX];
+#pragma unroll
+        for (int j = 0; j < LMAX; ++j) g[j] = 0.0;
         Mask<NW> v = diff;
 #pragma unroll
         for (int j = 0; j < LMAX; ++j) {  // the j-th flipped position, ascending
+#if BCHK_ACC_BREAK
+            if (!ballot(j < m)) break;  // no lane has a j-th flipped position
+#endif
             int pj = -1;
 #pragma unroll
             for (int s = NW - 1; s >= 0; --s)
@@ -1190,13 +1208,16 @@ __device__ __forceinline__ LaneRes<Geo<M>::NW> lane_decide(const uint8_t *ex, co
 #pragma unroll
             for (int s = 0; s < NW; ++s)
                 if ((pj >> 6) == s && pj >= 0) v.w[s] &= v.w[s] - 1;
-            g[j] = 0.0;
             if (pj >= 0) g[j] = yrow[pj];
         }
         l = 0.0;
 #pragma unroll
-        for (int j = 0; j < LMAX; ++j)
+        for (int j = 0; j < LMAX; ++j) {
+#if BCHK_ACC_BREAK
+            if (!ballot(j < m)) break;
+#endif
             if (j < m) l += fabs((2.0 * g[j]) / s2);
+        }
         double rs_lo = 0.0;
         int taken = 0;
 #pragma unroll
