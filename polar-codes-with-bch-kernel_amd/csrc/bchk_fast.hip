@@ -1286,7 +1286,6 @@ template <int M, int TMAX>
 __global__ void __launch_bounds__(kWaveSize * kLaneWaves) __attribute__((amdgpu_waves_per_eu(BCHK_LANE_WPE, BCHK_LANE_WPE)))
 kaneko_lane_kernel(SearchParams p) {
     constexpr int N = Geo<M>::N, NW = Geo<M>::NW;
-    constexpr int NSEG = (N + kLaneSeg - 1) / kLaneSeg;
     static_assert(kLaneSeg == 16, "segment = four rows of 16 positions per wave instruction");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     load_tables(smem, p.tables, p.td.bytes);
@@ -1324,19 +1323,34 @@ kaneko_lane_kernel(SearchParams p) {
     const uint32_t cw0 = 64u * gk, cw = cw0 + (uint32_t)lane;
     const bool live = cw < p.count;
     const uint32_t rows = p.count - cw0 < 64u ? p.count - cw0 : 64u;
-    // segment loads: instruction i, lane l -> row 4 i + l / 16, position 16 g + l % 16, as
-    // buffer loads over the chunk's rows (one lane offset, the row group in the scalar
-    // offset; rows past the batch read 0, position n -- the next row's first -- is unused)
+    // segment loads: instruction i, lane l -> row r = 4 i + l / 16, slot l % 16 of the row's
+    // segment g. Segments follow the 128-B lines, not the positions: row r's position 0 sits
+    // at 8-B slot a_r = (c0 + r N) mod 16 of its line, so segment g holds positions
+    // 16 g - a_r .. 16 g - a_r + 15, one whole line fetched once (position-aligned segments
+    // straddle two lines whose second half L2 had often dropped before the next segment
+    // asked for it: 1.6x the input read). Positions outside [0, n) are masked out; the
+    // offsets are all in the lane's VGPR (no scalar offset), so anything past the chunk's
+    // rows, or before them, is out of range and reads 0.
     const int lr = lane >> 4, lj = lane & 15;
     const __amdgpu_buffer_rsrc_t ysrc = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(p.y + (size_t)cw0 * N), (short)0, (int)(rows * (uint32_t)N * 8u), 0x00020000);
+    const uint32_t c0 = (uint32_t)(reinterpret_cast<uintptr_t>(p.y + (size_t)cw0 * N) >> 3) & 15u;
+    int vo[4];  // row 4 q + lr (and every 16th row on): its segment 0's offset (hi word)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = 4 * q + lr;
+        const int a = (int)((c0 + (uint32_t)(r * N)) & 15u);
+        vo[q] = (r * N + lj - a) * 8 + 4;
+    }
+    const int aself = (int)((c0 + (uint32_t)(lane * N)) & 15u);
+    constexpr int NSEG = (N + 15 + kLaneSeg - 1) / kLaneSeg;
     // (the keys and the hard decision need the hi words only: half the registers and LDS;
     // the acceptance tests read exact values from the rows again)
     uint32_t pf[16];
     auto load_seg = [&](int g) {
-        const int voff = (lr * N + kLaneSeg * g + lj) * 8 + 4;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) pf[i] = __builtin_amdgcn_raw_buffer_load_b32(ysrc, voff, i * 4 * N * 8, 0);
+        for (int i = 0; i < 16; ++i)
+            pf[i] = __builtin_amdgcn_raw_buffer_load_b32(ysrc, vo[i & 3] + kLaneSeg * 8 * g + (i >> 2) * 16 * N * 8, 0, 0);
     };
     load_seg(0);
     uint32_t kept[kLaneKeep];
@@ -1353,27 +1367,35 @@ kaneko_lane_kernel(SearchParams p) {
         for (int i = 0; i < 16; ++i) seg[(4 * i + lr) * kLaneRowD + lj] = pf[i];
         wave_sync();
         if (g + 1 < NSEG) load_seg(g + 1);
+        const int p0 = kLaneSeg * g - aself;  // this lane's first position of the segment
         uint32_t nk[16];
-        uint32_t sb = 0;  // sign bits of the segment (position 16 g + i -> bit i)
+        uint32_t sb = 0;  // sign bits of the segment (position p0 + i -> bit i)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const int pos = kLaneSeg * g + i;
+            const int pos = p0 + i;
+            const bool in = pos >= 0 && pos < N;
             const uint32_t hi = seg[lane * kLaneRowD + i];
-            nk[i] = pos < N ? sort_key8(hi, pos) : 0xFFFFFFFFu;
-            sb |= (pos < N ? (~hi >> 31) : 0u) << i;
+            nk[i] = in ? sort_key8(hi, pos) : 0xFFFFFFFFu;
+            sb |= (in ? (~hi >> 31) : 0u) << i;
         }
         sort16<0>(nk);
-        const int cnt = N - kLaneSeg * g > 16 ? 16 : N - kLaneSeg * g;
-        uint32_t top = nk[15];
+        // the real keys sort below the padding: the largest is rank cnt - 1
+        const int hiend = p0 + 16 < N ? p0 + 16 : N, loend = p0 > 0 ? p0 : 0;
+        const int cnt = hiend - loend;
+        uint32_t top = 0;
 #pragma unroll
-        for (int i = 0; i < 15; ++i) top = cnt == i + 1 ? nk[i] : top;
+        for (int i = 0; i < 16; ++i) top = cnt == i + 1 ? nk[i] : top;
         kmax_real = top > kmax_real ? top : kmax_real;
         merge_low32_16(kept, nk);
         // y > 0 is the clear sign bit (the hard decision, :336-342); y = +0 has prefix 0 and
-        // is sent to the slow path by lane_decide
+        // is sent to the slow path by lane_decide. Bits p0 .. p0 + 15 may span two words.
 #pragma unroll
-        for (int s = 0; s < NW; ++s)
-            yH.w[s] |= (g >> 2) == s ? (uint64_t)sb << (16 * (g & 3)) : 0ull;
+        for (int s = 0; s < NW; ++s) {
+            const int sh = p0 - 64 * s;
+            const uint64_t c = (sh >= 0 && sh < 64) ? (uint64_t)sb << (sh & 63)
+                             : (sh < 0 && sh > -16) ? (uint64_t)sb >> ((-sh) & 63) : 0ull;
+            yH.w[s] |= c;
+        }
     }
     // the kept keys into the (now free) row buffer, lane-major with stride 33 (conflict-free)
     wave_sync();

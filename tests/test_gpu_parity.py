@@ -723,10 +723,13 @@ def test_long_code_dense_redecode_handshake(long_rec):
         d.close()
 
 
-def _decode_count(d, y, tx, fill):
+def _decode_count(d, y, tx, fill, shift=0):
+    # shift: y starts `shift` doubles into its device buffer (rows off the 128-B lines)
     import torch
     B = y.shape[0]
-    dy, dtx = torch.from_numpy(y).cuda(), torch.from_numpy(tx).cuda()
+    buf = torch.zeros(y.size + 16, dtype=torch.float64, device="cuda")
+    buf[shift:shift + y.size] = torch.from_numpy(np.ascontiguousarray(y).reshape(-1)).cuda()
+    dy, dtx = buf[shift:], torch.from_numpy(tx).cuda()
     dres = torch.from_numpy(fill.copy()).cuda()
     dl0 = torch.zeros(B, dtype=torch.float64, device="cuda")
     c6 = torch.zeros(6, dtype=torch.int64, device="cuda")
@@ -736,14 +739,16 @@ def _decode_count(d, y, tx, fill):
     return dres.cpu().numpy(), dl0.cpu().numpy(), c6.cpu().numpy()
 
 
-@pytest.mark.parametrize("m,t,J,snr", [(8, 15, 15, 5.0), (8, 15, 15, 7.0), (8, 15, -1, 6.0), (7, 8, 15, 5.0),
-                                       (7, 6, -1, 7.0)])
-def test_lane_prepass_equals_first_kernel(m, t, J, snr):
+@pytest.mark.parametrize("m,t,J,snr,shift", [(8, 15, 15, 5.0, 0), (8, 15, 15, 7.0, 0), (8, 15, -1, 6.0, 0),
+                                             (7, 8, 15, 5.0, 0), (7, 6, -1, 7.0, 0), (8, 15, 15, 7.0, 5),
+                                             (7, 8, 15, 5.0, 11)])
+def test_lane_prepass_equals_first_kernel(m, t, J, snr, shift):
     # m >= 7 without a stats record: the lane-per-codeword pre-pass (kaneko_lane_kernel)
     # decides the rows that return at test pattern 0 or 1 and the first kernel skips them.
     # Decoded rows, l0 bits and the fused counters equal a context without the pre-pass,
     # on a ragged batch (partial last chunk) with edge rows (exact and prefix ties, tiny,
-    # huge and zero samples, a noiseless codeword) and rows never accepted (the caller's fill)
+    # huge and zero samples, a noiseless codeword) and rows never accepted (the caller's fill);
+    # shift > 0 places y off the 128-B lines (the pre-pass streams line-aligned segments)
     on = dec(m, t, J=J)
     off = _ctx_env(m, t, J, BCHK_LANE_PRE=0)
     try:
@@ -760,7 +765,7 @@ def test_lane_prepass_equals_first_kernel(m, t, J, snr):
         y[B - 1, n - 1] = -y[B - 1, 0] * (1 + 2.0 ** -50)
         y[130, 2] = -y[130, 2] * 2.0 ** -40              # tiny |y| at one position
         fill = (np.arange(B * n, dtype=np.uint64).reshape(B, n) % 3 == 0).astype(np.uint8)
-        a = _decode_count(on, y, tx, fill)
+        a = _decode_count(on, y, tx, fill, shift)
         b = _decode_count(off, y, tx, fill)
         np.testing.assert_array_equal(a[0], b[0])
         np.testing.assert_array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
