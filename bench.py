@@ -7,8 +7,14 @@ counters when N > 1). Inputs are the reference's own channel stream (minstd_rand
 libstdc++ distributions; rank r starts (2^31-2)/N draws after rank r-1 in it), generated on the host and resident in HBM
 before timing. Weak scaling: every rank decodes its own B codewords.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch G]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`--gpus N` without a launcher (no WORLD_SIZE in the environment) starts the N rank processes
+itself, before anything touches a GPU, and exits with their status; under torchrun `--gpus`
+must equal the world size. `--batch B` is per rank (weak scaling, the default);
+`--global-batch G` fixes the job's total instead (strong scaling: G / N codewords per rank),
+which is how config 5's 2^20 words fit eight ranks' shares of the minstd_rand0 period.
 
 Rank 0 prints one JSON line (driver contract) with `roofline` (HIP-event kernel time of
 the dominant kernel vs the 8 TB/s HBM roof at 9n+8 algorithmic bytes per codeword),
@@ -17,6 +23,7 @@ the dominant kernel vs the 8 TB/s HBM roof at 9n+8 algorithmic bytes per codewor
 on disjoint ranges of the same stream, on a bounded sample of the same workload).
 """
 import argparse
+import contextlib
 import json
 import os
 import subprocess
@@ -40,7 +47,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: the launcher's world size, 1 without one")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--m", type=int, default=6)
@@ -49,7 +57,10 @@ def parse():
     ap.add_argument("--points", default="4,5,6",
                     help="Eb/N0 points (dB) of the FER/throughput curve; '' = the headline only")
     ap.add_argument("--J", type=int, default=15, help="test-pattern cap; -1 = shipped (uncapped)")
-    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per rank (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="codewords of the whole job, split evenly over the ranks (strong "
+                         "scaling); 0 = --batch per rank")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the cpu_baseline sample (0 = skip)")
@@ -201,8 +212,17 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
     d_st = torch.empty((B, bchk.STATS_DTYPE.itemsize), dtype=torch.uint8, device=dev)
     d_step = torch.zeros(6, dtype=torch.int64, device=dev)
     d_cnt = torch.zeros(6, dtype=torch.int64, device=dev)
-    stream = torch.cuda.ExternalStream(dec.stream, device=dev)
-    torch.cuda.synchronize()
+    cuda = dev.type == "cuda"  # cpu only under BCHK_BENCH_STUB (plumbing tests)
+    stream = torch.cuda.ExternalStream(dec.stream, device=dev) if cuda else None
+
+    def on_stream():
+        return torch.cuda.stream(stream) if cuda else contextlib.nullcontext()
+
+    def device_sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    device_sync()
 
     def step():
         # everything below is enqueued on the decoder's stream (torch ops via ExternalStream)
@@ -223,7 +243,7 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
                                     d_step.data_ptr(), dec.stream)
         reduce_step(d_step, d_cnt, world, dist)
 
-    with torch.cuda.stream(stream):
+    with on_stream():
         for _ in range(args.warmup):
             step()
         dec.sync()
@@ -231,12 +251,12 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
         dec.sync()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        device_sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
         dec.sync()
-        torch.cuda.synchronize()
+        device_sync()
         elapsed = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
@@ -246,18 +266,18 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
         for _ in range(args.steps):
             step()
         dec.sync()
-        torch.cuda.synchronize()
+        device_sync()
     ms4, launches = dec.profile_read_stages()  # fast, exact first pass, coop, analytic tail
     dec.profile(False)
     # FER / op counters of the batch itself: every step re-decodes the same resident words,
     # so the counts come from ONE more step on zeroed counters (world * B distinct words)
-    with torch.cuda.stream(stream):
+    with on_stream():
         dec.sync()
         d_cnt.zero_()
         dec.sync()
         step()
         dec.sync()
-        torch.cuda.synchronize()
+        device_sync()
     n_exact, n_coop = dec.path_counts()
     n_tail = dec.tail_count()
     tail_stats = dec.tail_stats()
@@ -329,27 +349,97 @@ def run_point(args, bchk, dec, snr, world, rank, dist, dev):
     }
 
 
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n_ranks, argv):
+    """`bench.py --gpus N` run directly: start the N rank processes here (the torchrun
+    environment: RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on 127.0.0.1), wait for them and
+    return the job's exit status. Called before anything in this process touches a GPU; the
+    children are ordinary child processes (no exec), rank 0 prints the JSON line. A rank that
+    fails ends the others (by their own PIDs) so the job cannot hang on a dead peer."""
+    port = str(free_port())
+    procs = []
+    for r in range(n_ranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n_ranks),
+                   LOCAL_WORLD_SIZE=str(n_ranks), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, BCHK_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def rank_batch(args, world):
+    """Codewords this rank decodes per step: --batch (weak scaling) or --global-batch / N
+    (strong scaling; the total must split evenly)."""
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"--global-batch {args.global_batch} does not split over {world} ranks")
+        return args.global_batch // world, "strong"
+    return args.batch, "weak"
+
+
 def main():
     args = parse()
+    launched = "WORLD_SIZE" in os.environ
+    if args.gpus is not None and args.gpus > 1 and not launched:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
+    args.batch, scaling = rank_batch(args, world)
     import torch
     import torch.distributed as dist
 
     bchk = load_pkg()
-    # one rank per GPU; more ranks than GPUs (a rehearsal of the N > 1 path on one GPU, gloo)
-    # share them round-robin
-    gpu = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(gpu)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
+    stub = os.environ.get("BCHK_BENCH_STUB")
+    if stub:
+        # CPU plumbing tests only (tests/test_bench_spawn.py): the oracle stands in for the
+        # device decoder so the rank launch, stream ranges and counter exchange run without a
+        # GPU; the line says so and is no measurement
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from bench_stub import StubDecoder
+        if args.backend != "gloo":
+            raise SystemExit("BCHK_BENCH_STUB runs on the CPU: --backend gloo")
+        gpu, dev = None, torch.device("cpu")
+        if world > 1:
             dist.init_process_group("gloo")
-    dec = bchk.KanekoKernelProcessor(args.m, args.t, J=args.J, device=gpu)
+        dec = StubDecoder(args.m, args.t, J=args.J)
+    else:
+        # one rank per GPU; more ranks than GPUs (a rehearsal of the N > 1 path on one GPU,
+        # gloo only: RCCL refuses two ranks on one device) share them round-robin
+        ndev = max(1, torch.cuda.device_count())
+        if world > ndev and args.backend == "nccl":
+            raise SystemExit(f"{world} ranks on {ndev} GPUs: nccl (RCCL) needs one GPU per rank; "
+                             "--backend gloo rehearses several ranks per GPU")
+        gpu = local % ndev
+        torch.cuda.set_device(gpu)
+        if world > 1:
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            else:
+                dist.init_process_group("gloo")
+        dec = bchk.KanekoKernelProcessor(args.m, args.t, J=args.J, device=gpu)
+        dev = torch.device("cuda", gpu)
     n, B = dec.n, args.batch
-    dev = torch.device("cuda", gpu)
     snrs = [float(x) for x in args.points.split(",") if x.strip()] if args.points else []
     if args.snr not in snrs:
         snrs.append(args.snr)
@@ -376,7 +466,7 @@ def main():
             traffic = None
     if rank == 0:
         out = {
-            "metric": metric_name(n, dec.k, args.t, B),
+            "metric": metric_name(n, dec.k, args.t, world * B if scaling == "strong" else B),
             "value": round(head["value"], 3),
             "unit": "codewords/s",
             "n_gpus": world,
@@ -384,7 +474,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(head["ms_per_step"], 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: the reference's AWGN stream (minstd_rand0 + libstdc++ "
@@ -395,6 +485,8 @@ def main():
                        "code": f"BCH({n},{dec.k},{2 * args.t + 1})", "batch_per_gpu": B,
                        "global_batch": world * B, "snr_db": args.snr, "J": args.J,
                        "L_inert": 8, "parallelism": f"dp{world}",
+                       "launch": ("bench.py --gpus" if os.environ.get("BCHK_BENCH_SPAWNED") else
+                                  "torchrun" if launched else "single"),
                        "backend": args.backend if world > 1 else None},
             "fer": head["fer"],
             "ber": head["ber"],
@@ -424,9 +516,11 @@ def main():
             "host_generation_s": round(head["host_generation_s"], 2),
             "counters_complete": head["counters_complete"],
             **({"cut_build": True} if head["cut_build"] else {}),
+            **({"stub_decoder": "tests/bench_stub.py (CPU oracle, plumbing test; not a measurement)"}
+               if stub else {}),
             "rank_draws": head["rank_draws"], "rank_draw_budget": head["rank_draw_budget"],
         }
-        if world == 1:
+        if world == 1 and not stub:
             out["cpu_baseline"] = cpu_baseline(args, head["value"], bchk)
         print(json.dumps(out), flush=True)
     if world > 1:

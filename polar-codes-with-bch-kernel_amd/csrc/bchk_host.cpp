@@ -779,14 +779,24 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
     }
     if (p.heavy_tail) {
         if (c->m >= 7 && c->long_help && c->ks.long_job_bytes) {  // jobs of the cooperative workgroups
+            // A chunk record is taken as delivered when its tag equals (generation << 32 |
+            // chunk + 1), the generation built from this context's 20-bit launch epoch. Tags
+            // must therefore never hold a value from another context (memory hipMalloc hands
+            // back) or from the launch 2^20 epochs ago: the jobs memory is zeroed whenever it
+            // is (re)allocated and whenever the epoch's low 20 bits wrap. A zero tag matches
+            // no chunk (chunk + 1 >= 1).
+            const size_t jobs_cap_before = P.jobs.cap;  // ensure() only grows it
             if ((rc = P.jobctl.ensure((size_t)(grid_coop + 1) * 128)) ||
                 (rc = P.jobs.ensure((size_t)grid_coop * c->ks.long_job_bytes)))
                 return rc;
             HIP_TRY(hipMemsetAsync(P.jobctl.p, 0, (size_t)(grid_coop + 1) * 128, cs));
+            const uint32_t epoch = ++c->long_epoch;
+            if (P.jobs.cap != jobs_cap_before || (epoch & 0xFFFFFu) == 0u)
+                HIP_TRY(hipMemsetAsync(P.jobs.p, 0, P.jobs.cap, cs));
             pc.long_jobctl = P.jobctl.p;
             pc.long_jobs = P.jobs.p;
             pc.long_help_max = c->long_help_max;
-            pc.long_epoch = ++c->long_epoch;
+            pc.long_epoch = epoch;
             pc.long_share_min = c->long_share_min;
         }
         if (c->profile) HIP_TRY(hipEventRecord(ev.e[4], cs));
@@ -939,7 +949,15 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (const char *ti = getenv("BCHK_TAIL_INLINE")) c->tail_inline = atoi(ti) != 0;
     if (const char *ah = getenv("BCHK_AN_HELP")) c->an_help = atoi(ah) != 0;
     if (const char *fw = getenv("BCHK_FAST_RING_WAVES")) c->fast_waves = (uint32_t)std::max(2, std::min(16, atoi(fw)));
-    if (const char *fm = getenv("BCHK_FAST_MODE")) c->fast_mode = (uint32_t)std::max(0, atoi(fm));
+    if (const char *fm = getenv("BCHK_FAST_MODE")) {
+        c->fast_mode = (uint32_t)std::max(0, atoi(fm));
+#ifndef BCHK_EXPERIMENT_MODES
+        // modes 1 and 2 time parts of the ring kernel and give wrong results: experiment
+        // builds only, never the product library (a leftover variable must not yield a
+        // plausible-looking record)
+        if (c->fast_mode == 1u || c->fast_mode == 2u) c->fast_mode = 0;
+#endif
+    }
     if (const char *tb = getenv("BCHK_TAIL_BLOCKS")) c->tail_conc_blocks = std::max(1, atoi(tb));
     if (const char *tm = getenv("BCHK_TAIL_MIN_BOUND")) c->tail_min_bound = strtoull(tm, nullptr, 10);
     if (const char *hf = getenv("BCHK_HEAVY_FIRST")) c->heavy_first = atoi(hf) != 0;

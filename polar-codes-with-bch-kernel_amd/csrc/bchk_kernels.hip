@@ -942,12 +942,12 @@ kaneko_coop_kernel(SearchParams p) {
                         for (uint32_t j = (uint32_t)lane; j < gridDim.x; j += 64) {
                             const JobCtl *q = jcb + j;
                             if (j == blockIdx.x || g_ld32(&q->state) != 1u || g_ld32(&q->done) ||
-                                g_ld32(&q->helpers) >= kHelpersMax)
+                                g_ld32(&q->helpers) >= help_max)
                                 continue;
                             const uint64_t bch = (g_ld64(&q->bound) + 63ull) >> 6, nx = g_ld32(&q->next);
                             const uint64_t left = bch > nx ? bch - nx : 0ull;
                             const uint64_t kj = ((left < (1ull << 39) ? left : (1ull << 39) - 1ull) << 24) | j;
-                            if (left >= kShareMinChunks && kj > key) key = kj;
+                            if (left >= share_min && kj > key) key = kj;
                         }
 #pragma unroll
                         for (int o = 32; o; o >>= 1) {
