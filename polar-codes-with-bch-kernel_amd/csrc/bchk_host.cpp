@@ -989,6 +989,15 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     }
     if (c->ks.tail) c->grid_tail = grid_of(c->ks.tail_ptr(), kWaveSize * kWavesPerBlock, c->lds_tail);
     if (c->ks.tail_tab) c->grid_tail_tab = grid_of(c->ks.tail_tab_ptr(), kWaveSize * kWavesPerBlock, c->lds_tail);
+    if (const char *fp = getenv("BCHK_FIRST_PER_CU")) {  // experiment: the first pass's workgroups per CU
+        const int per = std::max(1, atoi(fp));
+        c->grid = per * prop.multiProcessorCount;
+        if (c->ks.search_tab) c->grid_tab = per * prop.multiProcessorCount;
+    }
+    if (getenv("BCHK_VERBOSE"))  // persistent grids (workgroups) and their LDS bytes
+        fprintf(stderr, "bchk m=%d t=%d cus=%d grid %d (lds %zu) tab %d (lds %zu) tail %d tail_tab %d (lds %zu) coop %d coop_tab %d (lds %zu)\n",
+                m, t, prop.multiProcessorCount, c->grid, c->lds, c->grid_tab, c->lds_tab, c->grid_tail,
+                c->grid_tail_tab, c->lds_tail, c->grid_coop, c->grid_coop_tab, c->lds_coop);
     (void)rc;
     *out = c;
     return 0;
