@@ -696,6 +696,9 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             HIP_TRY(hipMemsetAsync(c->tdiag.p, 0, c->tdiag.cap, s));
             q.tail_diag = (unsigned long long *)c->tdiag.p;
             q.tail_diag_cap = (uint32_t)(c->tdiag.cap / 128);
+#ifdef BCHK_FP_TRACE
+            q.tail_diag_count = ctrl + kTailStats + 16;  // first-pass timeline records first
+#endif
         }
         if (inl) {  // the analytic tail inside the first pass; failures to the cooperative kernel
             q.analytic = 1;

@@ -103,6 +103,14 @@ kaneko_search_kernel(SearchParams p) {
     uint32_t ndone = 0;
     for (;;) {
         uint32_t cw = kEmptySlot, item = 0;
+#ifdef BCHK_FP_TRACE
+        // diagnostic build (never the product): per-codeword timeline of the first pass on
+        // the 100 MHz clock into the tail diagnostics buffer, tagged 0xF in word 0's top nibble
+        // (scripts/fp_trace.py, profiles/r06_fp/)
+        uint64_t fpt[3] = {0, 0, 0};
+        const uint64_t fp_t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t fp_c0 = __builtin_amdgcn_s_memtime();
+#endif
         if (live) {
             if (lane == 0) cw = tail_dequeue(p, item);
             cw = (uint32_t)__shfl((int)cw, 0, 64);
@@ -129,7 +137,32 @@ kaneko_search_kernel(SearchParams p) {
             cw = p.queue[qi];
         }
         if (cw < p.count)  // never otherwise: no access outside the batch
+        {
+#ifdef BCHK_FP_TRACE
+            const uint64_t fp_t1 = __builtin_amdgcn_s_memrealtime();
+            search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item, help, wid,
+                                              AN ? nullptr : fpt);
+            if (!AN && p.tail_diag && p.tail_diag_count && lane == 0) {
+                const uint64_t fp_t4 = __builtin_amdgcn_s_memrealtime(), fp_c4 = __builtin_amdgcn_s_memtime();
+                const uint32_t r = atomicAdd(p.tail_diag_count, 1u);
+                if (r < p.tail_diag_cap) {
+                    unsigned long long *d = p.tail_diag + (size_t)r * 8;
+                    uint32_t hw;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                    d[0] = (0xFull << 60) | cw;
+                    d[1] = fp_t0;
+                    d[2] = fp_t1;
+                    d[3] = fpt[0];
+                    d[4] = fpt[1];
+                    d[5] = fp_t4;
+                    d[6] = fpt[2] | (uint64_t)xcc_id() << 20 | (uint64_t)hw << 32;
+                    d[7] = fp_c4 - fp_c0;
+                }
+            }
+#else
             search_codeword<M, TMAX, TAB, AN>(p, ex, lg, col, chien, as, ap, ordl, cw, lane, an, item, help, wid);
+#endif
+        }
         ++ndone;
     }
     wave_done(p, lane, ndone);

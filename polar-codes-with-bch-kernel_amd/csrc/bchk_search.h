@@ -1871,8 +1871,9 @@ template <int M, int TMAX, bool TAB, bool AN>
 __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const uint16_t *lg,
                                 const uint32_t *col, const uint64_t *chien, double *as,
                                 double *ap, uint8_t *ordl, uint32_t cw, int lane, AnWave *an,
-                                uint32_t item, HelpCtl *help, int wid) {
+                                uint32_t item, HelpCtl *help, int wid, uint64_t *fpt = nullptr) {
     constexpr int NW = Geo<M>::NW;
+    (void)fpt;  // BCHK_FP_TRACE (diagnostic builds): [0] prep done, [1] patterns done, [2] chunks
     // analytic tail: exact chunks end at an_stop, then the candidates decide the rest
     bool an_tried = false, an_exact = false;
     uint64_t an_stop = 0;
@@ -1907,6 +1908,9 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
     const TxPre<NW> txp = tx_prefetch<M>(p, cw, lane);
     Prep<M, TMAX> P;
     prep_codeword<M, TMAX>(p, col, as, ap, ordl, cw, lane, P);
+#ifdef BCHK_FP_TRACE
+    if (fpt) fpt[0] = __builtin_amdgcn_s_memrealtime();
+#endif
     FP_STAMP(0)
     if (AN && p.tail_diag) dg_t1 = __builtin_amdgcn_s_memtime();
     SearchState<NW> S;
@@ -2097,6 +2101,12 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         }
         FP_STAMP(2)
         if (handed) {
+#ifdef BCHK_FP_TRACE
+            if (fpt) {
+                fpt[1] = __builtin_amdgcn_s_memrealtime();
+                fpt[2] = chunks | 0x10000u;
+            }
+#endif
             fp_flush();
             tail_record();
             return;
@@ -2104,6 +2114,12 @@ __device__ void search_codeword(const SearchParams &p, const uint8_t *ex, const 
         if (S.done) break;
     }
     if (helped) help_close(help, lane, p);
+#ifdef BCHK_FP_TRACE
+    if (fpt) {
+        fpt[1] = __builtin_amdgcn_s_memrealtime();
+        fpt[2] = chunks;
+    }
+#endif
     write_outputs<M, TMAX>(S, P, p, cw, lane, txp);
     FP_STAMP(3)
     fp_flush();
