@@ -481,6 +481,9 @@ static_assert(BCHK_COOP_SLOTS <= 64, "ring flags are polled one slot per lane");
 // m >= 7: waves of the cooperative workgroup (1 acceptor + decoders). 12 waves = 3 per SIMD
 // leave each wave 168 VGPRs, which the packed decoder (Berlekamp-Massey and the split test
 // per lane) needs without spilling; at 16 waves (128 VGPRs) it spilled 184-332 B per lane.
+// (The helper path of round 5 spills 168 B per lane at 12 waves too. Round 6 measured 16
+// waves: BCH(255,139,31) 2^20, 5 dB J = 15 cooperative kernel 64.4 -> 62.0 ms but 6 dB J = inf
+// 1.05 -> 1.35 ms; 8 waves 73.9 / 0.99 ms -- 12 stays; profiles/r06_long/coop_waves.jsonl.)
 #ifndef BCHK_LONG_COOP_WAVES
 #define BCHK_LONG_COOP_WAVES 12
 #endif
