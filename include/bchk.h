@@ -294,6 +294,13 @@ int bchk_polar_decode_host(bchk_polar *pc, const float *llr, size_t B, uint8_t *
                            uint8_t *cw, float *metric, int32_t *count);
 int bchk_polar_decode_device(bchk_polar *pc, const float *d_llr, size_t B, uint8_t *d_info,
                              uint8_t *d_cw, float *d_metric, int32_t *d_count, void *stream);
+/* Codes with a search layer (a matrix kernel above 32, e.g. the 64 x 64 extended-BCH kernel):
+ * one codeword's list decode can take seconds, so a decode call is a series of kernel launches
+ * of about 50 ms each (environment BCHK_POLAR_BUDGET_MS; 0 = one launch per call): a codeword
+ * is suspended between two search items and resumed by the next launch, with identical
+ * results. Such a call returns when the batch is decoded (it synchronises its stream). The
+ * launches the last call took (1 for codes without a search layer or with the budget off). */
+int bchk_polar_last_launches(const bchk_polar *pc, uint64_t *launches);
 /* CMixedKernelEncoder::Encode (MixedKernelEncoder.cpp:142-177), host side: info [B][K] ->
  * codewords [B][N]. */
 int bchk_polar_encode_host(const bchk_polar *pc, const uint8_t *info, size_t B, uint8_t *cw);

@@ -38,7 +38,7 @@ EXPORTS = (
     "bchk_set_chunk_limit", "bchk_set_syndrome_table",
     "bchk_syndrome_table_query", "bchk_syndrome_table_info", "bchk_polar_create", "bchk_polar_create_kdir",
     "bchk_polar_destroy", "bchk_polar_params", "bchk_polar_decode_host", "bchk_polar_decode_device",
-    "bchk_polar_encode_host", "bchk_polar_sync", "bchk_polar_stream",
+    "bchk_polar_encode_host", "bchk_polar_sync", "bchk_polar_stream", "bchk_polar_last_launches",
     "bchk_kernel_ebch", "bchk_kernel_field_order", "bchk_kernel_trellis_cost", "bchk_kernel_column_costs",
     "bchk_kernel_column_search", "bchk_last_error", "bchk_version",
 )
@@ -432,6 +432,12 @@ class PolarListDecoder:
 
     def sync(self):
         _check(lib().bchk_polar_sync(self._h))
+
+    def last_launches(self):
+        """Kernel launches the last decode call took (time-budgeted codes with search layers)."""
+        n = C.c_uint64()
+        _check(lib().bchk_polar_last_launches(self._h, C.byref(n)))
+        return n.value
 
 
 def stream_skip(k, n, state, words):

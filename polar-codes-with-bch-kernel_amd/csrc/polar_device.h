@@ -52,6 +52,9 @@ constexpr int kPolarMaxTrellisKernel = 32;  // the trellis is built for kernels 
 constexpr int kMlStack = BCHK_ML_STACK;
 constexpr int kMlEnumBits = 10;
 constexpr uint32_t kMlScratchBytes = 12u * kMlStack + 8u * 64u + 8u * 65u + 8u + 4u * 64u + 4u * 64u;
+// the scratch before the stack (G, U, cost, ay: polar_mixed.hip MlScratch), saved with a
+// suspended search together with the stack's live nodes
+constexpr uint32_t kMlHeadBytes = 8u * 64u + 8u * 65u + 8u + 4u * 64u + 4u * 64u;
 // Matrix layers of size >= the trellis threshold (default 16, BCHK_POLAR_TRELLIS) take their
 // LLRs from CTrellisKernelProcessor's trellis (pull-form Viterbi over predecessor lists);
 // smaller ones enumerate the coset (2^(size - 1 - phase) words per LLR). Per (layer, phase):
@@ -83,7 +86,41 @@ struct PolarMixedParams {
     uint8_t trellis[kPolarMaxLayers];  // matrix layer decoded through its trellis
     uint8_t ml[kPolarMaxLayers];       // matrix layer decoded by the ordered-statistics search
     int32_t any_ml;                    // LDS holds the search scratch
+    // Time-budgeted launches (round 6; codes with search layers): a wave past `budget` ticks
+    // of the 100 MHz clock since its launch began suspends its codeword between two search
+    // items (its LDS state and registers to rsave, rstate[cw] = 1) and starts no other; the
+    // host launches again until `unfinished` stays 0. rstate: 0 not started, 1 suspended,
+    // 2 done. budget 0 (or rstate null): every codeword runs to its end in one launch.
+    uint32_t *rstate;
+    uint8_t *rsave;
+    uint32_t rstride;       // bytes of rsave per codeword (polar_mixed_save_bytes)
+    uint32_t *unfinished;   // codewords left suspended or not started by this launch
+    uint64_t budget;
+    int32_t no_mid;         // experiments: suspend between search items only (BCHK_POLAR_NO_MID)
 };
+
+// The kernel's LDS offsets (polar_mixed.hip), shared with the host's save-area size.
+struct PolarMixedLayout {
+    int o_S, o_C, o_O, o_ph, o_rows, o_act, o_tm;
+};
+__host__ __device__ inline PolarMixedLayout polar_mixed_layout(int U, int L, int ssize, int csize, int osize, int nl,
+                                                               int rec_words) {
+    PolarMixedLayout o;
+    o.o_S = (4 * U + 15) & ~15;
+    o.o_C = o.o_S + 4 * ssize * L;
+    o.o_O = o.o_C + csize * L;
+    o.o_ph = (o.o_O + osize * L + 15) & ~15;
+    o.o_rows = (o.o_ph + 2 * U + 15) & ~15;
+    o.o_act = o.o_rows + 8 * kPolarMaxKernel * nl;
+    o.o_tm = (o.o_act + 4 * L + 4 * L * rec_words + 15) & ~15;
+    return o;
+}
+// a suspended codeword: header (64 B), six registers per lane (64 x 24 B), then the LDS of
+// the list state: channel / S / C / O ([0, o_ph)) and act / rec ([o_act, o_tm))
+// (+ a suspended search's scratch: kMlScratchBytes)
+__host__ __device__ inline uint32_t polar_mixed_save_bytes(const PolarMixedLayout &o) {
+    return (uint32_t)((64 + 64 * 24 + o.o_ph + (o.o_tm - o.o_act) + kMlScratchBytes + 15) & ~15);
+}
 
 inline uint32_t polar_mixed_lds_bytes(int U, int L, int K, int ssize, int csize, int osize, int nl,
                                       int tstates, bool ml) {

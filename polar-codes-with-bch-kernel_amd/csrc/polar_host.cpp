@@ -95,6 +95,10 @@ struct bchk_polar {
     size_t lds = 0;
     int grid = 0;
     PBuf llr, info, cw, metric, count;
+    // time-budgeted launches of codes with search layers (PolarMixedParams::budget)
+    PBuf rstate, rsave, unfinished;
+    uint64_t budget_ticks = 0;  // 100 MHz ticks per launch, 0 = one launch per call
+    uint64_t launches_last = 0; // launches the last budgeted call took
 };
 
 namespace {
@@ -474,6 +478,13 @@ int bchk_polar_create_kdir(const char *spec, const char *kdir, int list_size, in
     }
     c->grid = per_cu * prop.multiProcessorCount;
     if (const char *g = getenv("BCHK_POLAR_GRID")) c->grid = std::max(1, atoi(g));
+    // codes with search layers: launches of at most ~50 ms (BCHK_POLAR_BUDGET_MS, 0 = one
+    // launch per call), so no launch holds the GPU for seconds
+    if (c->mixed && c->mp.any_ml) {
+        double ms = 50.0;
+        if (const char *b = getenv("BCHK_POLAR_BUDGET_MS")) ms = std::max(0.0, atof(b));
+        c->budget_ticks = (uint64_t)(ms * 1e5);  // s_memrealtime: 100 MHz
+    }
     if (getenv("BCHK_POLAR_DEBUG"))
         fprintf(stderr, "bchk_polar: U=%d L=%d lds=%zu per_cu=%d CUs=%d grid=%d\n", c->U, c->L, c->lds, per_cu,
                 prop.multiProcessorCount, c->grid);
@@ -488,9 +499,18 @@ void bchk_polar_destroy(bchk_polar *c) {
     c->cw.release();
     c->metric.release();
     c->count.release();
+    c->rstate.release();
+    c->rsave.release();
+    c->unfinished.release();
     if (c->d_tab) (void)hipFree(c->d_tab);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+int bchk_polar_last_launches(const bchk_polar *c, uint64_t *launches) {
+    if (!c || !launches) return pfail(BCHK_EINVAL, "NULL argument");
+    *launches = c->budget_ticks ? c->launches_last : 1;
+    return 0;
 }
 
 int bchk_polar_params(const bchk_polar *c, int *n, int *k, int *unshortened, int *list_size) {
@@ -545,7 +565,38 @@ int bchk_polar_decode_device(bchk_polar *c, const float *d_llr, size_t B, uint8_
         m.N = c->N;
         m.K = c->K;
         m.L = c->L;
-        PHIP_TRY(launch_polar_mixed(m, grid, c->lds, stream ? (hipStream_t)stream : c->stream));
+        hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+        if (!(m.any_ml && c->budget_ticks)) {
+            PHIP_TRY(launch_polar_mixed(m, grid, c->lds, s));
+            return 0;
+        }
+        // Codes with search layers: one codeword's list decode can run for seconds (every
+        // phase's search items in one wave), so the call is a series of launches of at most
+        // ~budget each (plus one search item): a wave suspends its codeword between two items
+        // past the budget and the next launch resumes it (same results, bit for bit: the
+        // state saved is the whole list state). The call returns when every codeword is done.
+        const PolarMixedLayout ol = polar_mixed_layout(c->U, c->L, m.ssize, m.csize, m.osize, m.nl, polar_rec_words(c->K));
+        const uint32_t stride = polar_mixed_save_bytes(ol);
+        int rc;
+        if ((rc = c->rstate.ensure(B * 4)) || (rc = c->rsave.ensure(B * (size_t)stride)) ||
+            (rc = c->unfinished.ensure(4)))
+            return rc;
+        PHIP_TRY(hipMemsetAsync(c->rstate.p, 0, B * 4, s));
+        m.rstate = (uint32_t *)c->rstate.p;
+        m.rsave = (uint8_t *)c->rsave.p;
+        m.rstride = stride;
+        m.unfinished = (uint32_t *)c->unfinished.p;
+        m.budget = c->budget_ticks;
+        m.no_mid = getenv("BCHK_POLAR_NO_MID") ? 1 : 0;
+        for (uint64_t launch = 0;; ++launch) {
+            PHIP_TRY(hipMemsetAsync(c->unfinished.p, 0, 4, s));
+            PHIP_TRY(launch_polar_mixed(m, grid, c->lds, s));
+            uint32_t left = 0;
+            PHIP_TRY(hipMemcpyAsync(&left, c->unfinished.p, 4, hipMemcpyDeviceToHost, s));
+            PHIP_TRY(hipStreamSynchronize(s));
+            c->launches_last = launch + 1;
+            if (left == 0) break;
+        }
         return 0;
     }
     PHIP_TRY(launch_polar(p, grid, c->lds, stream ? (hipStream_t)stream : c->stream));

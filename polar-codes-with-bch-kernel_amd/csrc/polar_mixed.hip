@@ -184,94 +184,128 @@ __device__ __forceinline__ void ml_metric2(uint64_t dis, uint64_t fix, const flo
     fx = ml_metric(fix, ay, l);
 }
 
+// A search suspended between two rounds (time-budgeted launches): the wave-uniform state
+// beside the scratch (G, U, cost, ay, the stack's first sp nodes), which the caller saves
+// and restores with it.
+struct MlResume {
+    int sp;
+    float best0, best1;
+    uint64_t hd, lrb;
+};
+
+// rs == null: the whole search in this call. Otherwise *resume says whether the scratch and
+// *rs hold a suspended search to continue, and past the deadline (t_launch + budget on the
+// 100 MHz clock), after at least one round of this call, the search stops between two rounds:
+// *rs filled, *suspended set, the return value meaningless.
 __device__ float ml_llr(const uint64_t *kr, int l, int loc, const float *src, const uint8_t *off, int d, int s,
-                        int lane, const MlScratch &ms) {
-    // the layer's LLRs with the known inputs' sign flips (:240-262), HD = Y < 0 (:270-276)
-    float a = 0.0f;
-    bool neg = false;
-    if (lane < l) {
-        const float v = src[lane * d + s];
-        const float yv = off[lane * d + s] ? -v : v;
-        neg = yv < 0.0f;
-        a = fabsf(yv);
-        ms.ay[lane] = a;
-    }
-    const uint64_t hd = __ballot(neg);
-    wsync();
-    const int nf = l - loc - 1;
+                        int lane, const MlScratch &ms, MlResume *rs = nullptr, bool resume = false,
+                        uint64_t t_launch = 0, uint64_t budget = 0, bool *suspended = nullptr) {
     const float kInf = __int_as_float(0x7F800000);
-    if (nf <= kMlEnumBits) {  // small coset: enumerated, words spread over the lanes
-        float b0 = kInf, b1 = kInf;
-        for (uint32_t v = (uint32_t)lane; v < (1u << nf); v += 64) {
-            uint64_t c = 0;
-            for (int r = 0; r < nf; ++r)
-                if ((v >> r) & 1u) c ^= kr[loc + 1 + r];
-            const float m0 = ml_metric(c ^ hd, ms.ay, l), m1 = ml_metric(c ^ hd ^ kr[loc], ms.ay, l);
-            b0 = m0 < b0 ? m0 : b0;
-            b1 = m1 < b1 ? m1 : b1;
-        }
-        return wave_minf(b1) - wave_minf(b0);
-    }
-    // positions by decreasing |y| (bitonic across the lanes; key: |y| bits, valid, position)
-    uint64_t key = lane < l ? (((uint64_t)__float_as_uint(a) << 8) | 0x80ull | (uint64_t)(63 - lane)) : 0ull;
-    for (int k = 2; k <= 64; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t o = shfl_xor64(key, j);
-            const bool desc = (lane & k) == 0, lower = (lane & j) == 0;
-            key = (lower == desc) ? (o > key ? o : key) : (o < key ? o : key);
-        }
-    const int pos = 63 - (int)(key & 63ull);
-    // Gauss-Jordan: lane i < nf holds row loc + 1 + i; pivots in decreasing |y|
-    uint64_t g = lane < nf ? kr[loc + 1 + lane] : 0ull;
-    bool used = false;
-    int t = 0, piv = 0;
-    for (int si = 0, np = 0; si < l && np < nf; ++si) {
-        const int p = __builtin_amdgcn_readlane(pos, si);
-        const uint64_t cand = __ballot(lane < nf && !used && ((g >> p) & 1ull));
-        if (!cand) continue;
-        const int r = (int)__builtin_ctzll(cand);
-        const uint64_t gr = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), r) << 32);
-        if (lane == r) {
-            used = true;
-            t = np;
-            piv = p;
-        } else if (lane < nf && ((g >> p) & 1ull)) {
-            g ^= gr;
-        }
-        ++np;
-    }
-    if (lane < nf) {  // found in decreasing |y|: index nf - 1 - t runs by increasing cost
-        ms.G[nf - 1 - t] = g;
-        ms.cost[nf - 1 - t] = ms.ay[piv];
-    }
-    // non-pivot positions; below a word that has taken rows up to i - 1, every non-pivot
-    // disagreement outside U[i] is fixed, so its |y| bounds the subtree from below too
-    uint64_t pm = lane < nf ? (1ull << piv) : 0ull;
-    for (int o = 1; o < 64; o <<= 1) pm |= shfl_xor64(pm, o);
-    const uint64_t lrb = ~pm & (l >= 64 ? ~0ull : ((1ull << l) - 1ull));
-    wsync();
-    if (lane <= nf) {
-        uint64_t u = 0ull;
-        for (int q = lane; q < nf; ++q) u |= ms.G[q] & lrb;
-        ms.U[lane] = u;
-    }
-    // the roots: the word of each half that matches the hard decision on the pivots
-    const uint64_t root0 = wave_xor64(lane < nf && ((hd >> piv) & 1ull) ? g : 0ull);
-    const uint64_t t1 = hd ^ kr[loc];
-    const uint64_t root1 = kr[loc] ^ wave_xor64(lane < nf && ((t1 >> piv) & 1ull) ? g : 0ull);
-    float best0 = ml_metric(root0 ^ hd, ms.ay, l), best1 = ml_metric(root1 ^ hd, ms.ay, l);
-    int sp = 0;
-    if (lane == 0) {
-        ms.stk[0] = ml_node(root0, 0.0f, 0, 0);
-        ms.stk[1] = ml_node(root1, 0.0f, 0, 1);
-    }
-    sp = 2;
-    wsync();
     const uint64_t lt = (1ull << lane) - 1ull;
+    const int nf = l - loc - 1;
+    uint64_t hd, lrb;
+    float best0, best1;
+    int sp;
+    if (rs && resume) {
+        hd = rs->hd;
+        lrb = rs->lrb;
+        best0 = rs->best0;
+        best1 = rs->best1;
+        sp = rs->sp;
+    } else {
+        // the layer's LLRs with the known inputs' sign flips (:240-262), HD = Y < 0 (:270-276)
+        float a = 0.0f;
+        bool neg = false;
+        if (lane < l) {
+            const float v = src[lane * d + s];
+            const float yv = off[lane * d + s] ? -v : v;
+            neg = yv < 0.0f;
+            a = fabsf(yv);
+            ms.ay[lane] = a;
+        }
+        hd = __ballot(neg);
+        wsync();
+        if (nf <= kMlEnumBits) {  // small coset: enumerated, words spread over the lanes
+            float b0 = kInf, b1 = kInf;
+            for (uint32_t v = (uint32_t)lane; v < (1u << nf); v += 64) {
+                uint64_t c = 0;
+                for (int r = 0; r < nf; ++r)
+                    if ((v >> r) & 1u) c ^= kr[loc + 1 + r];
+                const float m0 = ml_metric(c ^ hd, ms.ay, l), m1 = ml_metric(c ^ hd ^ kr[loc], ms.ay, l);
+                b0 = m0 < b0 ? m0 : b0;
+                b1 = m1 < b1 ? m1 : b1;
+            }
+            return wave_minf(b1) - wave_minf(b0);
+        }
+        // positions by decreasing |y| (bitonic across the lanes; key: |y| bits, valid, position)
+        uint64_t key = lane < l ? (((uint64_t)__float_as_uint(a) << 8) | 0x80ull | (uint64_t)(63 - lane)) : 0ull;
+        for (int k = 2; k <= 64; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const uint64_t o = shfl_xor64(key, j);
+                const bool desc = (lane & k) == 0, lower = (lane & j) == 0;
+                key = (lower == desc) ? (o > key ? o : key) : (o < key ? o : key);
+            }
+        const int pos = 63 - (int)(key & 63ull);
+        // Gauss-Jordan: lane i < nf holds row loc + 1 + i; pivots in decreasing |y|
+        uint64_t g = lane < nf ? kr[loc + 1 + lane] : 0ull;
+        bool used = false;
+        int t = 0, piv = 0;
+        for (int si = 0, np = 0; si < l && np < nf; ++si) {
+            const int p = __builtin_amdgcn_readlane(pos, si);
+            const uint64_t cand = __ballot(lane < nf && !used && ((g >> p) & 1ull));
+            if (!cand) continue;
+            const int r = (int)__builtin_ctzll(cand);
+            const uint64_t gr = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, r) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), r) << 32);
+            if (lane == r) {
+                used = true;
+                t = np;
+                piv = p;
+            } else if (lane < nf && ((g >> p) & 1ull)) {
+                g ^= gr;
+            }
+            ++np;
+        }
+        if (lane < nf) {  // found in decreasing |y|: index nf - 1 - t runs by increasing cost
+            ms.G[nf - 1 - t] = g;
+            ms.cost[nf - 1 - t] = ms.ay[piv];
+        }
+        // non-pivot positions; below a word that has taken rows up to i - 1, every non-pivot
+        // disagreement outside U[i] is fixed, so its |y| bounds the subtree from below too
+        uint64_t pm = lane < nf ? (1ull << piv) : 0ull;
+        for (int o = 1; o < 64; o <<= 1) pm |= shfl_xor64(pm, o);
+        lrb = ~pm & (l >= 64 ? ~0ull : ((1ull << l) - 1ull));
+        wsync();
+        if (lane <= nf) {
+            uint64_t u = 0ull;
+            for (int q = lane; q < nf; ++q) u |= ms.G[q] & lrb;
+            ms.U[lane] = u;
+        }
+        // the roots: the word of each half that matches the hard decision on the pivots
+        const uint64_t root0 = wave_xor64(lane < nf && ((hd >> piv) & 1ull) ? g : 0ull);
+        const uint64_t t1 = hd ^ kr[loc];
+        const uint64_t root1 = kr[loc] ^ wave_xor64(lane < nf && ((t1 >> piv) & 1ull) ? g : 0ull);
+        best0 = ml_metric(root0 ^ hd, ms.ay, l);
+        best1 = ml_metric(root1 ^ hd, ms.ay, l);
+        if (lane == 0) {
+            ms.stk[0] = ml_node(root0, 0.0f, 0, 0);
+            ms.stk[1] = ml_node(root1, 0.0f, 0, 1);
+        }
+        sp = 2;
+        wsync();
+    }
     // a guard only (the search tree is finite): past 2^20 rounds the LLR is NaN, never a hang
     for (uint32_t rounds = 0; sp > 0; ++rounds) {
         if (rounds >= (1u << 20)) return __int_as_float(0x7FC00000);
+        if (rs && rounds > 0 && __builtin_amdgcn_s_memrealtime() - t_launch > budget) {
+            rs->sp = sp;  // past the launch's deadline: stop between two rounds
+            rs->best0 = best0;
+            rs->best1 = best1;
+            rs->hd = hd;
+            rs->lrb = lrb;
+            *suspended = true;
+            return 0.0f;
+        }
         // the top n nodes, one per lane; n shrinks near the stack's end so that the pushes of a
         // round (at most 2 per node) and of one depth-first descent (< 64) always fit
         int n = sp < 64 ? sp : 64;
@@ -322,13 +356,9 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
     const int U = p.U, nl = p.nl, L = p.L, K = p.K;
     const int RW = polar_rec_words(K);
     // LDS: polar_mixed_lds_bytes (polar_device.h)
-    const int o_S = (4 * U + 15) & ~15;
-    const int o_C = o_S + 4 * p.ssize * L;
-    const int o_O = o_C + p.csize * L;
-    const int o_ph = (o_O + p.osize * L + 15) & ~15;
-    const int o_rows = (o_ph + 2 * U + 15) & ~15;
-    const int o_act = o_rows + 8 * kPolarMaxKernel * nl;
-    const int o_tm = (o_act + 4 * L + 4 * L * RW + 15) & ~15;
+    const PolarMixedLayout lo = polar_mixed_layout(U, L, p.ssize, p.csize, p.osize, nl, RW);
+    const int o_S = lo.o_S, o_C = lo.o_C, o_O = lo.o_O, o_ph = lo.o_ph, o_rows = lo.o_rows, o_act = lo.o_act,
+              o_tm = lo.o_tm;
     float *chan = reinterpret_cast<float *>(smem);
     float *S = reinterpret_cast<float *>(smem + o_S);
     uint8_t *C = smem + o_C;
@@ -358,22 +388,120 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
     MStack st;
     st.slot = 0;
     wsync();
+    // time-budgeted launches (PolarMixedParams::budget): this launch's start on the 100 MHz clock
+    const bool budgeted = p.budget != 0 && p.rstate != nullptr;
+    const uint64_t t_launch = __builtin_amdgcn_s_memrealtime();
+    auto expired = [&]() { return budgeted && __builtin_amdgcn_s_memrealtime() - t_launch > p.budget; };
     for (uint32_t cw = blockIdx.x; cw < p.B; cw += gridDim.x) {
-        const float *y = p.llr + (size_t)cw * p.N;  // LoadLLRs (MixedKernelEncoder.cpp:181-207)
-        for (int i = lane; i < U; i += 64) {
-            const int m = p.symmap[i];
-            chan[i] = m >= 0 ? y[m] : (m == -1 ? 100000.0f : 0.0f);
+        const uint32_t cst = budgeted ? __builtin_amdgcn_readfirstlane(p.rstate[cw]) : 0u;
+        if (cst == 2u) continue;  // finished by an earlier launch
+        if (expired()) {          // past the budget: start (or resume) nothing more
+            if (lane == 0) atomicAdd(p.unfinished, 1u);
+            continue;
         }
-        st.reset(L, lane);
-        const uint32_t pid = st.pop(lane);
-        uint32_t active = 1u << pid;
+        uint8_t *sv = budgeted ? p.rsave + (size_t)cw * p.rstride : nullptr;
+        uint32_t active;
         float R = 0.0f, lv = 0.0f;
         uint64_t dm = 0;
         uint32_t rw = 0;
-        int k = 0;
+        int k = 0, phi0 = 0, rj = -1, rit = 0;  // rj >= 0: resume in layer rj at item rit
+        if (cst == 1u) {
+            // resume a suspended codeword: header, registers, the list state's LDS
+            const uint32_t *hd = reinterpret_cast<const uint32_t *>(sv);
+            phi0 = (int)__builtin_amdgcn_readfirstlane(hd[0]);
+            rj = (int)__builtin_amdgcn_readfirstlane(hd[1]);
+            rit = (int)__builtin_amdgcn_readfirstlane(hd[2]);
+            k = (int)__builtin_amdgcn_readfirstlane(hd[3]);
+            active = __builtin_amdgcn_readfirstlane(hd[4]);
+            st.top = (int)__builtin_amdgcn_readfirstlane(hd[5]);
+            const uint32_t *rg = hd + 16 + 6 * lane;
+            R = __uint_as_float(rg[0]);
+            lv = __uint_as_float(rg[1]);
+            dm = (uint64_t)rg[2] | ((uint64_t)rg[3] << 32);
+            rw = rg[4];
+            st.slot = rg[5];
+            const uint8_t *ls = sv + 64 + 64 * 24;
+            for (int i = 4 * lane; i < o_ph; i += 256) *reinterpret_cast<uint32_t *>(smem + i) = *reinterpret_cast<const uint32_t *>(ls + i);
+            for (int i = 4 * lane; i < o_tm - o_act; i += 256)
+                *reinterpret_cast<uint32_t *>(smem + o_act + i) = *reinterpret_cast<const uint32_t *>(ls + o_ph + i);
+        } else {
+            const float *y = p.llr + (size_t)cw * p.N;  // LoadLLRs (MixedKernelEncoder.cpp:181-207)
+            for (int i = lane; i < U; i += 64) {
+                const int m = p.symmap[i];
+                chan[i] = m >= 0 ? y[m] : (m == -1 ? 100000.0f : 0.0f);
+            }
+            st.reset(L, lane);
+            const uint32_t pid = st.pop(lane);
+            active = 1u << pid;
+        }
         wsync();
         int nact = list_act(active);
-        for (int phi = 0; phi < U; ++phi) {
+        bool progressed = false, yielded = false;
+        // suspend between two search items (the list state is complete there: every layer
+        // before rj done, layer rj's offset state applied, items before it done)
+        MlResume mr{0, 0.0f, 0.0f, 0ull, 0ull};
+        bool rmid = false;  // resuming inside a search item (its scratch saved too)
+        if (cst == 1u) {
+            const uint32_t *hd = reinterpret_cast<const uint32_t *>(sv);
+            rmid = __builtin_amdgcn_readfirstlane(hd[6]) != 0u;
+            if (rmid) {
+                mr.sp = (int)__builtin_amdgcn_readfirstlane(hd[7]);
+                mr.best0 = __uint_as_float(__builtin_amdgcn_readfirstlane(hd[8]));
+                mr.best1 = __uint_as_float(__builtin_amdgcn_readfirstlane(hd[9]));
+                // (readfirstlane returns int: through uint32_t, or the low word sign-extends)
+                mr.hd = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(hd[10]) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(hd[11]) << 32);
+                mr.lrb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(hd[12]) |
+                         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(hd[13]) << 32);
+                const uint8_t *ml = sv + 64 + 64 * 24 + o_ph + (o_tm - o_act);
+                const int mb = (int)kMlHeadBytes + 12 * mr.sp;  // G, U, cost, ay, stack[0, sp)
+                for (int i = 4 * lane; i < mb; i += 256) *reinterpret_cast<uint32_t *>(mls + i) = *reinterpret_cast<const uint32_t *>(ml + i);
+                wsync();
+            }
+        }
+        // mid: inside a search item, whose scratch and MlResume go along
+        auto suspend = [&](int phi, int j, int it, bool mid) {
+            uint32_t *hd = reinterpret_cast<uint32_t *>(sv);
+            if (lane == 0) {
+                hd[0] = (uint32_t)phi;
+                hd[1] = (uint32_t)j;
+                hd[2] = (uint32_t)it;
+                hd[3] = (uint32_t)k;
+                hd[4] = active;
+                hd[5] = (uint32_t)st.top;
+                hd[6] = mid ? 1u : 0u;
+                hd[7] = (uint32_t)mr.sp;
+                hd[8] = __float_as_uint(mr.best0);
+                hd[9] = __float_as_uint(mr.best1);
+                hd[10] = (uint32_t)mr.hd;
+                hd[11] = (uint32_t)(mr.hd >> 32);
+                hd[12] = (uint32_t)mr.lrb;
+                hd[13] = (uint32_t)(mr.lrb >> 32);
+            }
+            if (mid) {
+                uint8_t *ml = sv + 64 + 64 * 24 + o_ph + (o_tm - o_act);
+                const int mb = (int)kMlHeadBytes + 12 * mr.sp;
+                for (int i = 4 * lane; i < mb; i += 256) *reinterpret_cast<uint32_t *>(ml + i) = *reinterpret_cast<const uint32_t *>(mls + i);
+            }
+            uint32_t *rg = hd + 16 + 6 * lane;
+            rg[0] = __float_as_uint(R);
+            rg[1] = __float_as_uint(lv);
+            rg[2] = (uint32_t)dm;
+            rg[3] = (uint32_t)(dm >> 32);
+            rg[4] = rw;
+            rg[5] = st.slot;
+            uint8_t *ls = sv + 64 + 64 * 24;
+            for (int i = 4 * lane; i < o_ph; i += 256) *reinterpret_cast<uint32_t *>(ls + i) = *reinterpret_cast<const uint32_t *>(smem + i);
+            for (int i = 4 * lane; i < o_tm - o_act; i += 256)
+                *reinterpret_cast<uint32_t *>(ls + o_ph + i) = *reinterpret_cast<const uint32_t *>(smem + o_act + i);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (lane == 0) {
+                p.rstate[cw] = 1u;
+                atomicAdd(p.unfinished, 1u);
+            }
+            yielded = true;
+        };
+        for (int phi = phi0; phi < U && !yielded; ++phi) {
             const uint32_t e = __builtin_amdgcn_readfirstlane((uint32_t)ph[phi]);
             // ---- IterativelyCalcS (KernelListEngine.cpp:370-447)
             int m = nl - 1;
@@ -383,6 +511,8 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                 --m;
             }
             for (int j = m; j < nl; ++j) {
+                if (rj >= 0 && j < rj) continue;  // done before the suspension
+                const bool resume_here = rj == j;
                 const int loc = (j == m) ? (int)(pq % (uint32_t)p.ksize[j]) : 0;
                 const int d = p.outer[j + 1], l = p.ksize[j];
                 const int tot = nact * d;
@@ -407,7 +537,7 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                 }
                 // matrix layer: offset state (:240-262), then the min-sum LLR per element
                 const uint64_t *kr = rows + kPolarMaxKernel * j;
-                for (int it = lane; it < tot; it += 64) {
+                for (int it = lane; it < tot && !resume_here; it += 64) {  // (applied before a suspension)
                     const int q = (int)act[it / d], s = it % d;
                     uint8_t *off = Oof(q, j);
                     if (!loc) {
@@ -423,12 +553,27 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                 if (p.ml[j]) {
                     // exact ordered-statistics search (kernels larger than the trellis limit):
                     // one item at a time, the whole wave on it
-                    for (int it = 0; it < tot; ++it) {
+                    for (int it = resume_here ? rit : 0; it < tot; ++it) {
+                        if (progressed && expired()) {  // past the launch's budget: suspend here
+                            suspend(phi, j, it, false);
+                            break;
+                        }
                         const int q = (int)act[it / d], s = it % d;
-                        const float v = ml_llr(kr, l, loc, Sof(q, j), Oof(q, j), d, s, lane, ms);
+                        const bool mid = resume_here && it == rit && rmid;  // continue a suspended search
+                        bool susp = false;
+                        const float v = ml_llr(kr, l, loc, Sof(q, j), Oof(q, j), d, s, lane, ms,
+                                               budgeted && !p.no_mid ? &mr : nullptr, mid, t_launch, p.budget,
+                                               &susp);
+                        if (susp) {  // the search itself ran past the budget: suspended inside it
+                            suspend(phi, j, it, true);
+                            break;
+                        }
                         if (lane == 0) Sof(q, j + 1)[s] = v;
                         wsync();
+                        progressed = true;
                     }
+                    rj = -1;
+                    if (yielded) break;
                     continue;
                 }
                 if (p.trellis[j]) {
@@ -523,6 +668,7 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                 }
                 wsync();
             }
+            if (yielded) break;
             const bool on = mine && ((active >> lane) & 1u);
             if (on) lv = Sof(lane, nl)[0];
             const uint64_t corr = (e & kPhaseCorr) ? p.dfcorr[phi] : 0ull;
@@ -621,6 +767,10 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
                 }
             }
         }
+        if (yielded) {  // suspended: outputs when it finishes in a later launch
+            wsync();
+            continue;
+        }
         if ((k & 31) && mine && ((active >> lane) & 1u)) rec[lane * RW + (k >> 5)] = rw;
         wsync();
         // ---- final order (:249-267): active paths by (R, index), descending
@@ -642,6 +792,7 @@ __global__ void __launch_bounds__(64) polar_mixed_kernel(PolarMixedParams p) {
             if (lane == 0) p.metric[row] = rdlf_m(R, q);
         }
         if (lane == 0) p.count[cw] = nact;
+        if (budgeted && lane == 0) p.rstate[cw] = 2u;
         wsync();
     }
 }

@@ -24,6 +24,8 @@ for name, K in KERNELS.items():
 B = int(os.environ.get("BENCH_B", "16384"))
 CASES = [(("bch64f",), 32, 8, 2.0), (("bch64f",), 32, 8, 3.0), (("bch64f",), 32, 1, 3.0), (("bch64f",), 32, 4, 3.0),
          (("A", "bch64f"), 64, 8, 2.5), (("bch64f", "A"), 64, 8, 2.5)]
+if os.environ.get("BENCH_CASES"):  # e.g. "0,4": a subset of CASES
+    CASES = [CASES[int(i)] for i in os.environ["BENCH_CASES"].split(",")]
 for layers, K, L, snr in CASES:
     spec = mixed_spec(layers, K, dyn=0, seed=1)
     o = PolarOracle(spec, kdir)
@@ -34,7 +36,7 @@ for layers, K, L, snr in CASES:
     t0 = time.perf_counter()
     got = d.decode(llr)
     g = time.perf_counter() - t0
-    n_cpu = 16
+    n_cpu = int(os.environ.get("BENCH_CPU", "16"))
     t0 = time.perf_counter()
     want = o.decode_batch(llr[:n_cpu], L, threads=1)
     c = time.perf_counter() - t0
@@ -43,4 +45,5 @@ for layers, K, L, snr in CASES:
     print(json.dumps({"layers": "-".join(layers), "N": o.N, "K": K, "L": L, "snr_db": snr, "B": B,
                       "gpu_cw_s": round(B / g, 1), "oracle_cw_s_1core": round(n_cpu / c, 3),
                       "ratio": round((B / g) / (n_cpu / c), 1), "fer_best_path": fer,
-                      "same_as_oracle": same}), flush=True)
+                      "same_as_oracle": same, "launches": d.last_launches(),
+                      "budget_ms": os.environ.get("BCHK_POLAR_BUDGET_MS", "50 (default)")}), flush=True)

@@ -166,3 +166,32 @@ def test_gpu_64x64_kernel_matches_oracle(kdir, layers, K, dyn, punct, L):
     for snr in (1.0, 3.0):
         llr = awgn_llr(cw, snr, K / o.N, seed=int(snr * 10) + L)
         _same(d.decode(llr), o.decode_batch(llr, L))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("budget_ms", ["1", "20"])
+def test_gpu_64x64_budgeted_launches_equal_one_launch(kdir, budget_ms, monkeypatch):
+    # A decode call over the 64 x 64 kernel is a series of launches of ~budget each: codewords
+    # are suspended between two search items and resumed by the next launch. Lists, metrics and
+    # counts equal one unbounded launch bit for bit (and the oracle), and the call did take
+    # several launches.
+    layers, K, dyn, punct = CODES64[0]
+    spec = mixed_spec(layers, K, dyn, punct, seed=len(layers) * 19 + K)
+    o = PolarOracle(spec, kdir)
+    L = 8
+    rng = np.random.default_rng(61)
+    info = rng.integers(0, 2, (24, K)).astype(np.uint8)
+    llr = awgn_llr(o.encode(info), 2.0, K / o.N, seed=62)
+    monkeypatch.setenv("BCHK_POLAR_BUDGET_MS", "0")
+    one = load().PolarListDecoder(spec, L, kernel_dir=kdir)
+    a = one.decode(llr)
+    assert one.last_launches() == 1
+    monkeypatch.setenv("BCHK_POLAR_BUDGET_MS", budget_ms)
+    many = load().PolarListDecoder(spec, L, kernel_dir=kdir)
+    b = many.decode(llr)
+    print(f"\nbudget {budget_ms} ms: {many.last_launches()} launches")
+    assert many.last_launches() > 1
+    _same(b, a)
+    _same(b, o.decode_batch(llr, L))
+    b2 = many.decode(llr[::-1].copy())  # state of a previous call is not reused
+    _same(b2, o.decode_batch(llr[::-1].copy(), L))
