@@ -447,7 +447,7 @@ def main():
     head = pts[args.snr]
     dom = next(k for k in head["kernels"] if k["name"] == head["dominant_kernel"])
     # HBM bytes per launch of the dominant kernel, from the committed PMC passes of the same
-    # workload (scripts/gpu_final5.sh -> scripts/traffic_req_json.py, rocprofv3 --pmc memory-
+    # workload (scripts/gpu_final6.sh -> scripts/traffic_req_json.py, rocprofv3 --pmc memory-
     # side requests by size); null when no profile of this workload exists. It is a stored
     # measurement (rocprofv3 cannot run inside this process): its source is named. A stage of
     # two launches (lane pre-pass + first kernel) sums both.

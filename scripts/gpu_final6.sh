@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-5 artefacts: all GPU tests, the default bench line (CPU baseline), rocprofv3 kernel
+# Round-6 artefacts: all GPU tests, the default bench line (CPU baseline), rocprofv3 kernel
 # stats and memory-side traffic (PMC requests by size) of the headline; optionally (CONFIG5=1) config 5's lines with
 # their PMC traffic and CPU baseline. Every GPU step under its own limit; stops at a failure.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
-TAG=${1:-final5}
+TAG=${1:-final6}
 mkdir -p $OUT
 cd $ROOT
 if [ -z "${SKIP_TESTS:-}" ]; then
@@ -33,6 +33,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
     -- python3 $ROOT/bench.py --cpu-seconds 0 --points 5 > $OUT/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $ROOT
+# bench.py --gpus 2 without a launcher: it spawns its two ranks (gloo: both on the box's one GPU)
+timeout -k 10 300 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --points '' --cpu-seconds 0 > $OUT/bench2_$TAG.json 2> $OUT/bench2_$TAG.err
+rc=$?; echo "bench --gpus 2 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 [ -n "${CONFIG5:-}" ] || exit 0
 : > $OUT/${TAG}_255.jsonl
 for PT in "5 15" "6 -1" "7 15"; do
