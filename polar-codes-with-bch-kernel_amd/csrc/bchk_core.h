@@ -254,7 +254,7 @@ __device__ __forceinline__ void bm_locator_g(const GF &gf, const uint32_t *Sw, i
             const int r = 2 * k;
             int lC[TMAX + 1];
             // C_i = 0 for i > 2k - 1 before step k (deg C <= L <= 2k - 1): their logs are the
-            // zero sentinel without a table lookup (56 of the 240 lookups at TMAX = 15)
+            // zero sentinel without a table lookup (71 of the 240 lookups at t = TMAX = 15)
 #pragma unroll
             for (int i = 0; i <= TMAX; ++i) lC[i] = (i <= 2 * k - 1 || i == 0) ? gf.lg(C[i]) : gf.zl();
             // before step k, deg C <= L <= 2k-1; after it, deg C <= 2k+1 (terms beyond are
