@@ -151,6 +151,13 @@ __device__ __forceinline__ uint32_t gf_exp2(const uint8_t *ex, int la, int lb) {
 //     into the packed table (the cooperative kernel's LDS array was 88 % busy, half of it
 //     in bank conflicts, r05 PMC). handle = 64 log + 4 r, so a product is one
 //     v_add3 (a + b - 4 r) and one ds_read_b32, as before one add and one ds_read_u8.
+//   GfMul (m >= 7, the cooperative kernel's decoders, round 6): the whole product table
+//     [2^m][2^m] (64 KiB at m = 8) and the inverses in LDS; handle = the element itself, so
+//     lg() is free and a product is one lookup. The decoders' log lookups go away: Berlekamp-
+//     Massey re-logs C at every step (169 of its ~520 lookups at t = 15), the split test
+//     logs every coefficient it squares or reduces by (~120 of ~1 050).
+// Besides the products: val(h) = the element of handle h; pdiv(b) / div_by(a, pdiv(b)) =
+// a / b with the divisor's part computed once (a log for the log views, its inverse for GfMul).
 template <int M>
 struct GfPlain {
     static constexpr int N = Geo<M>::N, ZL = Geo<M>::ZL;
@@ -158,6 +165,9 @@ struct GfPlain {
     const uint16_t *lg_;
     __device__ __forceinline__ int lg(uint32_t g) const { return lg_[g]; }
     __device__ __forceinline__ uint32_t mul(int a, int b) const { return gf_exp2<M>(ex, a, b); }
+    __device__ __forceinline__ uint32_t val(int h) const { return gf_exp2<M>(ex, h, 0); }
+    __device__ __forceinline__ int pdiv(int b) const { return b; }
+    __device__ __forceinline__ int div_by(int a, int pb) const { return div(a, pb); }
     __device__ __forceinline__ int zl() const { return ZL; }
     __device__ __forceinline__ int one() const { return 0; }
     __device__ __forceinline__ bool is_zl(int h) const { return h == ZL; }
@@ -183,6 +193,9 @@ struct GfRep {
     __device__ __forceinline__ uint32_t mul(int a, int b) const {
         return *reinterpret_cast<const uint32_t *>(rep + (a + b - lo));
     }
+    __device__ __forceinline__ uint32_t val(int h) const { return mul(h, one()); }
+    __device__ __forceinline__ int pdiv(int b) const { return b; }
+    __device__ __forceinline__ int div_by(int a, int pb) const { return div(a, pb); }
     __device__ __forceinline__ int zl() const { return ZL * S + lo; }
     __device__ __forceinline__ int one() const { return lo; }
     __device__ __forceinline__ bool is_zl(int h) const { return h == ZL * S + lo; }
@@ -194,7 +207,26 @@ struct GfRep {
         const int s2 = 2 * h - lo;
         return s2 >= N * S + lo ? s2 - N * S : s2;
     }
-    __device__ __forceinline__ int plain(int h) const { return (h - lo) / S; }
+    // any lane's handle (64 log + 4 r, 4 r < 64): the log alone
+    __device__ __forceinline__ int plain(int h) const { return h / S; }
+};
+template <int M>
+constexpr int gf_mul_bytes() { return (1 << (2 * M)) + (1 << M); }  // products, then inverses
+template <int M>
+struct GfMul {
+    const uint8_t *mt;    // LDS: mt[a 2^m + b] = a b, then iv[a] = 1 / a (iv[0] = 0)
+    const uint16_t *lg_;  // the packed log table (plain logs for the Chien scan)
+    __device__ __forceinline__ int lg(uint32_t g) const { return (int)g; }
+    __device__ __forceinline__ uint32_t mul(int a, int b) const { return mt[(a << M) | b]; }
+    __device__ __forceinline__ uint32_t val(int h) const { return (uint32_t)h; }
+    __device__ __forceinline__ int zl() const { return 0; }
+    __device__ __forceinline__ int one() const { return 1; }
+    __device__ __forceinline__ bool is_zl(int h) const { return h == 0; }
+    __device__ __forceinline__ int pdiv(int b) const { return mt[(1 << (2 * M)) + b]; }
+    __device__ __forceinline__ int div_by(int a, int pb) const { return mt[(a << M) | pb]; }
+    __device__ __forceinline__ int div(int a, int b) const { return div_by(a, pdiv(b)); }
+    __device__ __forceinline__ int dbl(int h) const { return mt[(h << M) | h]; }  // h^2
+    __device__ __forceinline__ int plain(int h) const { return lg_[h]; }
 };
 // fills the replicated tables from the packed ones (a whole workgroup, before a barrier)
 template <int M>
@@ -566,10 +598,11 @@ template <int M, int TMAX, class GF>
 __device__ __forceinline__ bool split_test(const GF &gf, const int (&lc)[TMAX + 1], int deg, bool act) {
     static_assert(TMAX >= 2, "split test needs TMAX >= 2");
     int lq[TMAX];
+    const int pc0 = gf.pdiv(lc[0]);
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) {  // q_j = C_(TMAX - j) / C_0
         const int v = lc[TMAX - j];
-        lq[j] = gf.is_zl(v) ? v : gf.div(v, lc[0]);
+        lq[j] = gf.is_zl(v) ? v : gf.div_by(v, pc0);
     }
     // x^(2P) for the largest power of two P <= TMAX - 1 (so 2P >= TMAX): x^TMAX = q, then
     // 2P - TMAX multiplications by x; then squarings up to x^(2^m)
@@ -578,7 +611,7 @@ __device__ __forceinline__ bool split_test(const GF &gf, const int (&lc)[TMAX + 
     static_assert(SQ >= 1, "2P < 2^m");
     uint32_t g[TMAX];
 #pragma unroll
-    for (int j = 0; j < TMAX; ++j) g[j] = gf.mul(lq[j], gf.one());
+    for (int j = 0; j < TMAX; ++j) g[j] = gf.val(lq[j]);
 #pragma unroll
     for (int e = TMAX; e < 2 * P; ++e) mulx_mod<M, TMAX>(gf, lq, g);
 #pragma unroll
@@ -625,9 +658,6 @@ __device__ __forceinline__ bool alg_decode_lanes_g(const GF &gf, const uint8_t *
 #else
     if (ballot(ok)) ok = split_test<M, TMAX>(gf, lc, deg, ok) && ok;
 #endif
-    // the Chien scan below reads the packed exp table with plain logs
-#pragma unroll
-    for (int i = 0; i <= TMAX; ++i) lc[i] = gf.plain(lc[i]);
 #pragma unroll
     for (int s = 0; s < NW; ++s) E.w[s] = 0;
     for (uint64_t sm = ballot(ok); sm; sm &= sm - 1) {
@@ -645,7 +675,9 @@ __device__ __forceinline__ bool alg_decode_lanes_g(const GF &gf, const uint8_t *
 #pragma unroll
         for (int i = 0; i <= TMAX; ++i) {
             if (i <= dg) {
-                const int lti = __builtin_amdgcn_readlane(lc[i], src);
+                // the scan reads the packed exp table: plain logs (a lookup for GfMul, only
+                // for the rare successful lanes)
+                const int lti = gf.plain(__builtin_amdgcn_readlane(lc[i], src));
 #pragma unroll
                 for (int s = 0; s < NW; ++s) {
                     v[s] ^= gf_exp2<M>(ex, lti, ik[s]);

@@ -76,6 +76,9 @@ struct SearchParams {
     // its hard-decision syndrome table: [ceil(n/8)][256][W] words, entry (j, v) = the
     // syndrome of byte value v at positions 8j .. 8j + 7
     const uint32_t *syn8;
+    // m >= 7: GF(2^m) products [2^m][2^m] then inverses [2^m] (bytes), which the
+    // cooperative kernel stages into LDS for its decoders (GfMul, bchk_core.h)
+    const uint8_t *gfmul;
     // heavy codewords: the wave kernel hands a codeword still running after chunk_limit
     // steps of 64 patterns to the cooperative kernel, which may run concurrently with it
     // (heavy_tail == null disables the hand-off). Longest-first: codewords whose loop bound

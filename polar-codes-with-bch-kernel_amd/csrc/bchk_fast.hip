@@ -100,20 +100,28 @@ __device__ __forceinline__ void merge_low16_2(uint32_t (&kept)[16], const uint32
 
 // 32-bit sort key: a monotone 26-bit prefix of |y| (5 exponent bits covering
 // [2^-27, 2^5) + 21 mantissa bits) above the 6-bit position. |y| below the range maps to
-// prefix 0 or 1, above it (and inf/NaN) to the all-ones prefix; both are detected after the sort.
-// Five VALU operations: the biased exponent minus 996 saturates at 0 (|y| < 2^-27 then gives
-// prefix 0 or 1 -- the lo word's top bit -- and prefixes <= 1 are sent to the slow path), the
-// funnel shift appends the 21st mantissa bit, and the min saturates |y| >= 32 / inf / NaN.
+// prefix 0, above it (and inf/NaN) to the all-ones prefix; both are detected after the sort.
+// Four VALU operations: the funnel shift drops the sign and appends the 21st mantissa bit
+// ((hi:lo) >> 31 = |y|'s top 32 bits below the sign), the biased exponent minus 996 (in that
+// shifted form) saturates at 0 (|y| < 2^-27: prefix 0, sent to the slow path like every
+// prefix <= 1), and the min saturates |y| >= 32 / inf / NaN.
 __device__ __forceinline__ uint32_t sort_key(uint32_t hi, uint32_t lo, int pos) {
-    const uint32_t ahi = hi & 0x7FFFFFFFu;
-    const uint32_t d = __builtin_elementwise_sub_sat(ahi, (uint32_t)(1023 - 27) << 20);
-    const uint32_t mid = __builtin_amdgcn_alignbit(d, lo, 31);  // (d:lo) >> 31 = d << 1 | lo >> 31
+    const uint32_t top = __builtin_amdgcn_alignbit(hi, lo, 31);  // hi << 1 | lo >> 31
+    const uint32_t mid = __builtin_elementwise_sub_sat(top, (uint32_t)(1023 - 27) << 21);
     const uint32_t pre = mid < 0x3FFFFFFu ? mid : 0x3FFFFFFu;
     return (pre << 6) | (uint32_t)pos;
 }
 
 // the hard decision yH = (2y/s2 > 0) (:336-342) from the sign bits shifted in from the top
 // (yHl: positions 0..31, yHh: 32..N-1, last position at bit 31)
+template <int N>
+__device__ __forceinline__ uint64_t hard_decision(uint32_t yHl, uint32_t yHh);
+// the same from sign bits shifted in from the bottom, one funnel shift per position
+// (yH = yH << 1 | hi >> 31: the last position at bit 0): bit-reversed, they are the above
+template <int N>
+__device__ __forceinline__ uint64_t hard_decision_rev(uint32_t yHl, uint32_t yHh) {
+    return hard_decision<N>(__builtin_bitreverse32(yHl), __builtin_bitreverse32(yHh));
+}
 template <int N>
 __device__ __forceinline__ uint64_t hard_decision(uint32_t yHl, uint32_t yHh) {
     if constexpr (N < 32) {
@@ -344,7 +352,11 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
     }
     between();
     const bool need1 = live && !bad && !ok0 && !zero0;
+#ifdef BCHK_FAST_NO_I1  // experiment builds: the i = 1 decode left to the exact kernels
+    if (false) {
+#else
     if (ballot(need1)) {
+#endif
         uint32_t S1[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) S1[w] = S0[w] ^ col[o0 * W + w];
@@ -744,8 +756,8 @@ kaneko_fast_ring_kernel(SearchParams p) {
                             const uint64_t bb = (uint64_t)__double_as_longlong(v8[i]);
                             const uint32_t hi = (uint32_t)(bb >> 32), lo = (uint32_t)bb;
                             nk[8 * h + i] = sort_key(hi, lo, pos);
-                            if (pos < 32) yHl = (yHl >> 1) | (hi & 0x80000000u);
-                            else yHh = (yHh >> 1) | (hi & 0x80000000u);
+                            if (pos < 32) yHl = __builtin_amdgcn_alignbit(yHl, hi, 31);
+                            else yHh = __builtin_amdgcn_alignbit(yHh, hi, 31);
                         } else {
                             nk[8 * h + i] = 0xFFFFFFFFu;
                         }
@@ -796,7 +808,7 @@ kaneko_fast_ring_kernel(SearchParams p) {
         };
         const bool hold = full && p.fast_mode == 3u;
         if (!hold) release();
-        const uint64_t yH = hard_decision<N>(yHl, yHh);
+        const uint64_t yH = hard_decision_rev<N>(yHl, yHh);
         if (p.fast_mode == 2u) {  // experiment: the rows' path alone (wrong results)
             if (hold) release();
             if (p.l0 && live) p.l0[cw] = (double)(kept[3] ^ kmax_real ^ (uint32_t)yH);

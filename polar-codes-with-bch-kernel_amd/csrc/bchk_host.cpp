@@ -445,6 +445,7 @@ struct bchk_ctx {
     uint32_t long_help_max = 0, long_share_min = 0;
     uint32_t long_epoch = 0;  // cooperative launches with jobs (tag generations)  // BCHK_LONG_HELP_MAX / BCHK_LONG_SHARE_MIN (0: defaults)
     DevBuf syn8;  // its hard-decision syndrome table (SearchParams::syn8)
+    DevBuf gfmul; // m >= 7: GF(2^m) products and inverses (SearchParams::gfmul)
     int tail_conc_blocks = 64;     // blocks of the concurrent tail kernel (BCHK_TAIL_BLOCKS)
     bool heavy_first = true;       // fast path queues likely heavy codewords first (BCHK_HEAVY_FIRST)
     // hybrid tail: a first-pass hand-off whose loop bound is below this goes to a cooperative
@@ -598,6 +599,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
     p.J = c->J;
     p.variant = variant;
     p.fault = (uint32_t *)c->fault.p;
+    p.gfmul = (const uint8_t *)c->gfmul.p;  // null for m <= 6
     if (d_tx) {  // fused counters (zeroed by launch_search at allocation, then by every reduction)
         p.tx = d_tx;
         p.cnt = (unsigned long long *)c->cnt.p;
@@ -937,6 +939,20 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
             return fail(BCHK_EHIP, "device setup failed: %s", hipGetErrorString(hipGetLastError()));
         }
     }
+    if (c->ks.gfmul) {
+        // the cooperative decoders' product table: [a][b] = a b, then [a] = 1 / a (0 for 0)
+        const int q = 1 << m, n = c->field.n;
+        std::vector<uint8_t> mt((size_t)q * q + q, 0);
+        for (int a = 1; a < q; ++a)
+            for (int b = 1; b < q; ++b)
+                mt[(size_t)a * q + b] = (uint8_t)c->field.alog[(c->field.log[a] + c->field.log[b]) % n];
+        for (int a = 1; a < q; ++a) mt[(size_t)q * q + a] = (uint8_t)c->field.alog[(n - c->field.log[a]) % n];
+        if (c->gfmul.ensure(mt.size()) != 0 ||
+            hipMemcpy(c->gfmul.p, mt.data(), mt.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            bchk_destroy(c);
+            return fail(BCHK_EHIP, "device setup failed: %s", hipGetErrorString(hipGetLastError()));
+        }
+    }
     if (const char *lp = getenv("BCHK_LANE_PRE")) c->lane_pre = atoi(lp) != 0;
     if (const char *lh = getenv("BCHK_LONG_HELP")) c->long_help = atoi(lh) != 0;
     if (const char *hm = getenv("BCHK_LONG_HELP_MAX")) c->long_help_max = (uint32_t)std::max(1, atoi(hm));
@@ -1024,6 +1040,7 @@ void bchk_destroy(bchk_ctx *c) {
     c->synd.release();
     c->ok.release();
     c->syn8.release();
+    c->gfmul.release();
     if (c->d_tables) (void)hipFree(c->d_tables);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

@@ -441,9 +441,19 @@ kaneko_first_kernel(SearchParams p) {
 // 9.9, + 4-chunk claims in the last 60 chunks 81.1-81.6 / 9.8-9.9, 384 slots 81.1 / 9.7;
 // profiles/r04_long/coop_ring*.jsonl). Round 5, with helper workgroups (the ring is also the
 // window of chunks helpers may run ahead): 256 slots 64.2 / 1.57 ms, 512 64.2 / 1.17, 1024
-// 64.3 / 1.07 (profiles/r05_long/help_ring_slots.jsonl)
+// 64.3 / 1.07 (profiles/r05_long/help_ring_slots.jsonl). With the decoders' product table
+// (BCHK_LONG_GFMUL, 64 KiB of LDS at m = 8) 1024 slots (123 KiB at m = 8) no longer fit: 512.
+// The decoders' GF arithmetic (m >= 7): 0 = log / exp tables (GfPlain), 1 = the product
+// table (GfMul: no log lookups, ~18 % fewer lookups per test word). Measured (round 6,
+// profiles/r06_long/coop_gfmul_rejected.jsonl): cooperative kernel 5 dB J = 15 64.6 -> 89.8
+// ms, 6 dB J = inf 1.05 -> 1.63 ms. Random byte lookups spread over 64 KiB meet more bank
+// conflicts than sums of two logs into the 1-KiB exp table, where lanes often share a dword
+// (a broadcast), so the product table is an experiment build only (make gm1).
+#ifndef BCHK_LONG_GFMUL
+#define BCHK_LONG_GFMUL 0
+#endif
 #ifndef BCHK_LONG_SLOTS
-#define BCHK_LONG_SLOTS 1024
+#define BCHK_LONG_SLOTS (BCHK_LONG_GFMUL ? 512 : 1024)
 #endif
 #ifndef BCHK_LONG_TAIL
 #define BCHK_LONG_TAIL 60
@@ -491,6 +501,11 @@ static_assert(BCHK_COOP_SLOTS <= 64, "ring flags are polled one slot per lane");
 #ifndef BCHK_LONG_GFREP
 #define BCHK_LONG_GFREP 0
 #endif
+static_assert(!(BCHK_LONG_GFREP && BCHK_LONG_GFMUL), "one GF view for the packed decoders");
+template <int M>
+constexpr size_t coop_gf_bytes() {
+    return BCHK_LONG_GFREP ? (size_t)gf_rep_bytes<M>() : BCHK_LONG_GFMUL ? (size_t)gf_mul_bytes<M>() : 0;
+}
 template <int M>
 constexpr int coop_waves() { return Geo<M>::NW > 1 ? BCHK_LONG_COOP_WAVES : kCoopWaves; }
 static_assert(kLongSlots <= kCoopSlotsMax && kLongSlots >= (BCHK_LONG_COOP_WAVES - 1) * kLongClaim + 8,
@@ -541,7 +556,7 @@ template <int M, int TMAX>
 constexpr size_t coop_wave_area() {
     return Geo<M>::NW == 1 ? (size_t)kCoopWaves * Smem<M, TMAX>::WAVE_BYTES
                            : (size_t)Smem<M, TMAX>::WAVE_BYTES + (size_t)coop_waves<M>() * kCoopScratch +
-                                 (BCHK_LONG_GFREP ? (size_t)gf_rep_bytes<M>() : 0) + sizeof(PrepTab<M, TMAX>);
+                                 coop_gf_bytes<M>() + sizeof(PrepTab<M, TMAX>);
 }
 
 struct CoopCtl {
@@ -892,10 +907,17 @@ kaneko_coop_kernel(SearchParams p) {
     uint8_t *wscr = area + Smem<M, TMAX>::WAVE_BYTES + wid * kCoopScratch;  // m >= 7
     uint8_t *grep = area + Smem<M, TMAX>::WAVE_BYTES + coop_waves<M>() * kCoopScratch;  // m >= 7
     PrepTab<M, TMAX> *ptab =
-        reinterpret_cast<PrepTab<M, TMAX> *>(grep + (BCHK_LONG_GFREP ? gf_rep_bytes<M>() : 0));  // m >= 7
+        reinterpret_cast<PrepTab<M, TMAX> *>(grep + coop_gf_bytes<M>());  // m >= 7
     if constexpr (NW > 1 && BCHK_LONG_GFREP) {
         __syncthreads();  // the packed tables are in LDS
         gf_rep_fill<M>(grep, ex, lg);
+    }
+    if constexpr (NW > 1 && BCHK_LONG_GFMUL) {
+        // the product table from HBM (built by the host; L2-resident after the first CU)
+        static_assert(gf_mul_bytes<M>() % 4 == 0, "dwords");
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(p.gfmul);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(grep);
+        for (int i = (int)threadIdx.x; i < gf_mul_bytes<M>() / 4; i += (int)blockDim.x) dst[i] = src[i];
     }
     double *as = reinterpret_cast<double *>(wbase);
     double *ap = as + NP;
@@ -926,6 +948,8 @@ kaneko_coop_kernel(SearchParams p) {
         const int lane = lane_o, tt = uni(t_o);
 #if BCHK_LONG_GFREP
         const GfRep<M> gfr{grep, 4 * (lane & 15)};
+#elif BCHK_LONG_GFMUL
+        const GfMul<M> gfr{grep, lg};
 #else
         const GfPlain<M> gfr{ex, lg};
 #endif
@@ -1759,6 +1783,7 @@ static KernelSet make_set() {
     }
     k.coop_threads = kWaveSize * coop_waves<M>();
     k.long_job_bytes = Geo<M>::NW > 1 ? sizeof(JobData<M, TMAX>) : 0;
+    k.gfmul = Geo<M>::NW > 1 && BCHK_LONG_GFMUL;
     k.coop_bytes = coop;
     k.alg = &launch_alg_impl<M, TMAX>;
     k.tmax = TMAX;

@@ -32,6 +32,7 @@ struct KernelSet {
     size_t tail_block_bytes;  // the block's helper-job control (HelpCtl) after the waves
     int coop_threads;         // the cooperative kernel's workgroup size
     size_t long_job_bytes;    // m >= 7: one job's data (SearchParams::long_jobs), 0 otherwise
+    bool gfmul;               // the cooperative kernel reads SearchParams::gfmul (BCHK_LONG_GFMUL builds)
 };
 
 typedef hipError_t (*FastFn)(const SearchParams &, size_t, hipStream_t);
