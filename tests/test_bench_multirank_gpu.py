@@ -33,15 +33,12 @@ def free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("m,t,snr", [(6, 6, 5.0)])
-def test_bench_two_ranks_gloo_counters_equal_shards(m, t, snr):
-    import torch
-    B = 1 << 16
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py",
-           "--gpus", "2", "--backend", "gloo", "--steps", "3", "--warmup", "1", "--batch", str(B),
-           "--points", "", "--cpu-seconds", "0"]  # BCH(63,30,13) at 5 dB: bench.py's defaults
-    # (no --m / --t: torch.distributed.run's parser would take them as abbreviations of its own)
+BENCH_ARGS = ["--gpus", "2", "--backend", "gloo", "--steps", "3", "--warmup", "1", "--points", "",
+              "--cpu-seconds", "0"]  # BCH(63,30,13) at 5 dB: bench.py's defaults
+# (no --m / --t: torch.distributed.run's parser would take them as abbreviations of its own)
+
+
+def run_two_ranks(cmd):
     env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
     out = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600, env=env)
     assert out.returncode == 0, out.stderr[-4000:]
@@ -49,6 +46,30 @@ def test_bench_two_ranks_gloo_counters_equal_shards(m, t, snr):
     assert len(lines) == 1, out.stdout  # rank 0 prints one line
     rec = json.loads(lines[0])
     print(json.dumps({k: rec[k] for k in ("value", "ms_per_step", "n_gpus", "config")}))
+    return rec
+
+
+@pytest.mark.parametrize("m,t,snr", [(6, 6, 5.0)])
+def test_bench_two_ranks_gloo_counters_equal_shards(m, t, snr):
+    B = 1 << 16
+    rec = run_two_ranks([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                         "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py",
+                         *BENCH_ARGS, "--batch", str(B)])
+    assert rec["config"]["launch"] == "torchrun"
+    check_counters_equal_shards(rec, m, t, snr, B)
+
+
+def test_bench_gpus2_spawns_its_ranks_counters_equal_shards():
+    """`python bench.py --gpus 2` with no launcher: bench.py starts both ranks itself (the
+    driver's scaling command without torchrun), one line, the two shards' counters."""
+    B = 1 << 16
+    rec = run_two_ranks([sys.executable, "bench.py", *BENCH_ARGS, "--batch", str(B)])
+    assert rec["config"]["launch"] == "bench.py --gpus"
+    check_counters_equal_shards(rec, 6, 6, 5.0, B)
+
+
+def check_counters_equal_shards(rec, m, t, snr, B):
+    import torch
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 2 * B
     assert rec["config"]["backend"] == "gloo" and rec["config"]["parallelism"] == "dp2"
     assert rec["value"] > 0 and rec["points"][0]["words"] == 2 * B
