@@ -145,7 +145,16 @@ struct FastRes {
     uint64_t best;
     double l0;
     bool bad, ok0, zero0;
+    bool heavy;  // unresolved, likely to run >= 127 test patterns (queue order only)
 };
+// An unresolved codeword whose hard decision decodes (ok0) runs to the loop bound of that
+// first improvement, (1 << T) - 1 with T from calcT's scan (:110-126, :383-390), unless a
+// later improvement moves it (rare). T estimated from the keys of ranks 0..15 (lower bounds
+// of alpha) at or above this flags the codeword for the front of the exact kernel's queue, so
+// the first pass starts it early (its last starters set its length). Queue order only: every
+// result is unchanged. 2^18 words at 5 dB (oracle): the estimate equals the true T for every
+// such word up to T = 9; a list-scheduling model of the first pass, 350 -> 280 us.
+constexpr int kHeavyT = 7;
 
 // Sort of the 64 keys (positions N..63 all-ones) into the 16 smallest in order, k[0..15].
 // SEL (no per-codeword stats requested, 2 TMAX + 2 <= 16): only the 16 smallest keys are
@@ -329,13 +338,51 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
     R.state = 0;  // 0 unresolved, 1 returned at i = 0, 2 returned at i = 1
     R.best = 0;
     R.l0 = DBL_MAX;
+    R.heavy = false;
     Mask<1> E;
     const bool ok0 = alg_core<M, TMAX>(ex, lg, chien, S0, t, E);
+    double lE = 0.0;
     if (!bad && ok0) {
-        double l;
         bool ret;
-        accept(rd0, E.w[0], l, ret);
-        if (ret) { R.state = 1; R.best = E.w[0]; R.l0 = l; }
+        accept(rd0, E.w[0], lE, ret);
+        if (ret) { R.state = 1; R.best = E.w[0]; R.l0 = lE; }
+    }
+    // ---- the loop bound of an unresolved ok0 codeword, estimated (queue order, FastRes::heavy):
+    // calcT(j) = the first t - (m + m0) / 2 agreeing sorted alphas + alpha of ranks j .. j + t,
+    // m = m0 = |E|; T = the first j with l < calcT(j). Ranks up to 15 from the keys.
+    if (ballot(live && !bad && ok0 && R.state == 0)) {
+        constexpr int RK = 16;
+        double al[RK];
+#pragma unroll
+        for (int r = 0; r < RK; ++r) {
+            const uint32_t pr = k[r] >> 6;
+            const uint64_t bits = ((uint64_t)((pr >> 21) + (1023u - 27u)) << 52) | ((uint64_t)(pr & 0x1FFFFFu) << 31);
+            al[r] = __longlong_as_double((long long)bits) * c2;
+        }
+        int need = t - __popcll(E.w[0]);
+        double A = 0.0;
+#pragma unroll
+        for (int r = 0; r < RK; ++r) {
+            const bool ag = !((E.w[0] >> (k[r] & 63u)) & 1ull);
+            if (ag && need > 0) {
+                A += al[r];
+                --need;
+            }
+        }
+        int T = RK - t;  // past the keys: at least this
+        bool found = false;
+#pragma unroll
+        for (int j = RK - 1; j >= 0; --j) {  // the first j with l < calcT(j), scanned from the top
+            double Wj = A;
+#pragma unroll
+            for (int i = 0; i <= TMAX; ++i)
+                if (j + i < RK && i <= t) Wj += al[j + i];
+            const bool below = j + t < RK && lE < Wj;
+            T = below ? j : T;
+            found = found || below;
+        }
+        (void)found;
+        R.heavy = live && !bad && ok0 && R.state == 0 && T >= kHeavyT;
     }
     // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371). When the
     // hard decision is a codeword (zero syndrome, which the decoder rejects), pattern 1 flips
@@ -424,7 +471,7 @@ __device__ __forceinline__ void fast_finish(const SearchParams &p, uint32_t cw, 
     const bool unres = live && R.state == 0;
     const uint64_t um = ballot(unres);
     if (um && p.qfront) {
-        const bool hv = unres && !R.bad && !R.ok0 && !R.zero0;
+        const bool hv = unres && ((!R.bad && !R.ok0 && !R.zero0) || R.heavy);
         const uint64_t hm = ballot(hv), om = um & ~hm;
         const uint64_t below = (1ull << lane) - 1ull;
         uint32_t bf = 0, bb = 0;
