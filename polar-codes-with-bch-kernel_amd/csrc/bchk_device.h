@@ -153,6 +153,7 @@ struct SearchParams {
     // more bytes, measured)
     uint32_t fast_waves;
     uint32_t fast_mode;
+    uint32_t heavy_t;  // fast path: estimated loop-bound exponent sending an ok0 codeword to the front (0: kHeavyT)
     // cooperative kernel, m >= 7: candidate records a ring slot keeps (0..2; a chunk with more
     // is decoded again densely on the acceptor's request), and its counters (null = off):
     // [0] dense re-decodes served, [1] heavy codewords started

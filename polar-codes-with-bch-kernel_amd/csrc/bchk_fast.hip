@@ -215,7 +215,8 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
                                                const uint64_t *chien, const uint32_t *k, uint32_t kmax_real,
                                                bool bad, uint64_t yH, Rd0 rd0, Rd1 rd1, Between between,
                                                bool live, int t, double s2, const uint32_t *lo = nullptr,
-                                               bool have_lo = false, const uint32_t *syn8 = nullptr) {
+                                               bool have_lo = false, const uint32_t *syn8 = nullptr,
+                                               int heavy_t = kHeavyT) {
     constexpr int N = Geo<M>::N;
     constexpr int W = (TMAX + 3) / 4;
     // calcRightSide takes the first border = 2t+1-m agreeing sorted positions; with m0 == m
@@ -382,7 +383,7 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
             found = found || below;
         }
         (void)found;
-        R.heavy = live && !bad && ok0 && R.state == 0 && T >= kHeavyT;
+        R.heavy = live && !bad && ok0 && R.state == 0 && T >= heavy_t;
     }
     // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371). When the
     // hard decision is a codeword (zero syndrome, which the decoder rejects), pattern 1 flips
@@ -869,7 +870,7 @@ kaneko_fast_ring_kernel(SearchParams p) {
         const FastRes R = fast_decide<M, TMAX>(
             ex, lg, col, chien, kept, kmax_real, false, yH, [&](int pos) { return hold ? lrow[pos] : yrow[pos]; },
             [&](int pos) { return yrow[pos]; }, [&] { if (hold) release(); }, live, t, s2,
-            lo, use_lo, p.syn8);
+            lo, use_lo, p.syn8, p.heavy_t ? (int)p.heavy_t : kHeavyT);
 
         // ---- outputs
         const bool resolved = live && R.state != 0;
