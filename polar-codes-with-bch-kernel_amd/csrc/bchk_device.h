@@ -154,6 +154,7 @@ struct SearchParams {
     uint32_t fast_waves;
     uint32_t fast_mode;
     uint32_t heavy_t;  // fast path: estimated loop-bound exponent sending an ok0 codeword to the front (0: kHeavyT)
+    uint32_t heavy_tmax;  // ... and at most this one (0: no upper limit; experiments)
     // cooperative kernel, m >= 7: candidate records a ring slot keeps (0..2; a chunk with more
     // is decoded again densely on the acceptor's request), and its counters (null = off):
     // [0] dense re-decodes served, [1] heavy codewords started

@@ -216,7 +216,7 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
                                                bool bad, uint64_t yH, Rd0 rd0, Rd1 rd1, Between between,
                                                bool live, int t, double s2, const uint32_t *lo = nullptr,
                                                bool have_lo = false, const uint32_t *syn8 = nullptr,
-                                               int heavy_t = kHeavyT) {
+                                               int heavy_t = kHeavyT, int heavy_tmax = 64) {
     constexpr int N = Geo<M>::N;
     constexpr int W = (TMAX + 3) / 4;
     // calcRightSide takes the first border = 2t+1-m agreeing sorted positions; with m0 == m
@@ -383,7 +383,7 @@ __device__ __forceinline__ FastRes fast_decide(const uint8_t *ex, const uint16_t
             found = found || below;
         }
         (void)found;
-        R.heavy = live && !bad && ok0 && R.state == 0 && T >= heavy_t;
+        R.heavy = live && !bad && ok0 && R.state == 0 && T >= heavy_t && T <= heavy_tmax;
     }
     // ---- i = 1: only where i = 0 failed (firstDecodingSuccessful = false, :371). When the
     // hard decision is a codeword (zero syndrome, which the decoder rejects), pattern 1 flips
@@ -870,7 +870,7 @@ kaneko_fast_ring_kernel(SearchParams p) {
         const FastRes R = fast_decide<M, TMAX>(
             ex, lg, col, chien, kept, kmax_real, false, yH, [&](int pos) { return hold ? lrow[pos] : yrow[pos]; },
             [&](int pos) { return yrow[pos]; }, [&] { if (hold) release(); }, live, t, s2,
-            lo, use_lo, p.syn8, p.heavy_t ? (int)p.heavy_t : kHeavyT);
+            lo, use_lo, p.syn8, p.heavy_t ? (int)p.heavy_t : kHeavyT, p.heavy_tmax ? (int)p.heavy_tmax : 64);
 
         // ---- outputs
         const bool resolved = live && R.state != 0;

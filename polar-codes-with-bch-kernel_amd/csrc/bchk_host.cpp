@@ -438,6 +438,7 @@ struct bchk_ctx {
     // mode (BCHK_FAST_MODE)
     uint32_t fast_waves = 0, fast_mode = 0;
     uint32_t heavy_t = 0;  // BCHK_HEAVY_T (experiments; 0: the kernel's kHeavyT)
+    uint32_t heavy_tmax = 0;  // BCHK_HEAVY_TMAX (experiments; 0: no upper limit)
     // m >= 7: the lane-per-codeword pre-pass of the first kernel (BCHK_LANE_PRE=0: off)
     FastFn lane = nullptr;
     bool lane_pre = true;
@@ -670,6 +671,7 @@ int launch_pipe(bchk_ctx *c, bchk_ctx::Pipe &P, bool first, int variant, const d
             f.fast_waves = c->fast_waves;
             f.fast_mode = c->fast_mode;
             f.heavy_t = c->heavy_t;
+            f.heavy_tmax = c->heavy_tmax;
             f.syn8 = (const uint32_t *)c->syn8.p;  // null unless built
         }
         if (lane) {
@@ -971,6 +973,7 @@ int bchk_create(int m, int t, int J, double decoder_snr_db, int device, bchk_ctx
     if (const char *ah = getenv("BCHK_AN_HELP")) c->an_help = atoi(ah) != 0;
     if (const char *fw = getenv("BCHK_FAST_RING_WAVES")) c->fast_waves = (uint32_t)std::max(2, std::min(16, atoi(fw)));
     if (const char *ht = getenv("BCHK_HEAVY_T")) c->heavy_t = (uint32_t)std::max(0, atoi(ht));
+    if (const char *hx = getenv("BCHK_HEAVY_TMAX")) c->heavy_tmax = (uint32_t)std::max(0, atoi(hx));
     if (const char *fm = getenv("BCHK_FAST_MODE")) {
         c->fast_mode = (uint32_t)std::max(0, atoi(fm));
 #ifndef BCHK_EXPERIMENT_MODES
